@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""Self-play positions/sec — Connect4 7x6, 200 sims/move, 4096 concurrent games per GPU.
+
+BASELINE.json metric "self-play positions/sec (Connect4, 200 sims/move) at
+1/2/4/8 MI355X" on configs[1]: ResNet-128 (ResidualTower filter_factor=32,
+num_blocks=20, random init, torch.manual_seed(0)), bf16 leaf evaluation.
+
+A *step* is one ply of every game slot of every rank: 200 PUCT simulations
+(select -> ResNet -> expand/backup) per game, then the move, Move records,
+env step and tree reuse (engine.SelfPlayEngine.ply).  Finished games are
+refilled immediately (steady state); after every ply the episode statistics
+are all-reduced over ranks and finished games' Move records are gathered to
+rank 0 (the replay owner), as in the north star.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       torchrun --nproc-per-node N bench.py --gpus N ...
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+# MI355X reference figures (/opt/skills/guides/MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+BF16_DENSE_PEAK_TFLOPS = 2500.0
+
+
+def resnet_flops_per_leaf(W, H, A, filter_factor, num_blocks):
+    """Dense FLOPs (2 x MAC) of one ResidualTower forward (games/general/modules.py:88-107)."""
+    C, ff, cells = 4 * filter_factor, filter_factor, W * H
+    conv3 = 2 * 9 * C * C * cells
+    f = 2 * 9 * 3 * C * cells + 2 * num_blocks * conv3
+    f += 2 * (2 * C * ff * cells)  # two 1x1 head convs
+    f += 2 * ff * cells * A + 2 * ff * cells * 8 * ff + 2 * 8 * ff
+    return f
+
+
+def select_bytes(sims, levels, A=7):
+    """Algorithmic HBM bytes moved by k_select.
+
+    Per scored level: the child block (A x {n i32, w f64, p f32, child i32}) + vmask + the
+    node's child index = 20A + 8.  Per simulation: tree header (active id, root id/board/
+    player, noise flag, A noise doubles, root n/w) + Philox state load/store = 86 + 8A + 128,
+    leaf record writes (16 per path entry + 38).
+    """
+    per_level = 20 * A + 8 + 16
+    per_sim = 86 + 8 * A + 128 + 38
+    return levels * per_level + sims * per_sim
+
+
+def cpu_baseline(seconds, cores, sims, filter_factor, num_blocks):
+    """The oracle (sequential Python MCTS restatement, numpy RNG) + the reference-architecture
+    ResNet in fp32 on host cores: one Connect4 game from the empty board, complete moves
+    only, for about `seconds`.  Same tree semantics as the reference's sequential search
+    (games/algos/mcts.py); no multiprocessing/IPC."""
+    import numpy as np
+    import torch
+
+    from oracle.mcts import NumpyRNG, OracleTree
+    from self_play_reinforcement_learning_amd.modules import ResidualTower
+
+    torch.set_num_threads(cores)
+    torch.manual_seed(0)
+    net = ResidualTower(7, 6, 7, num_blocks=num_blocks, filter_factor=filter_factor).eval()
+    np.random.seed(0)
+    with torch.no_grad():
+        tree = OracleTree("connect4", net, NumpyRNG(), sims)
+        env_player = 1
+        from oracle.envs import Connect4Env
+
+        env = Connect4Env()
+        t0 = time.time()
+        moves = 0
+        while time.time() - t0 < seconds:
+            a = tree.move()
+            tree.play_action(a)
+            _, r, done, _ = env.step(a, env_player)
+            moves += 1
+            env_player = -env_player
+            if done:
+                env.reset()
+                tree = OracleTree("connect4", net, NumpyRNG(), sims)
+                env_player = 1
+        dt = time.time() - t0
+    return dict(value=moves / dt, unit="positions/s", cores=cores, kind="port",
+                sample=f"oracle sequential MCTS ({sims} sims/move, numpy RNG) + ResNet-{4 * filter_factor}x{num_blocks} "
+                       f"fp32 torch CPU, 1 Connect4 game from the empty board, {moves} complete moves in {dt:.1f} s")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=8, help="timed plies")
+    ap.add_argument("--warmup", type=int, default=3, help="untimed plies")
+    ap.add_argument("--games", type=int, default=4096, help="concurrent games per GPU")
+    ap.add_argument("--sims", type=int, default=200)
+    ap.add_argument("--filter-factor", type=int, default=32)
+    ap.add_argument("--blocks", type=int, default=20)
+    ap.add_argument("--bucket", type=int, default=256)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gather", action="store_true", help="skip the rank-0 Move gather")
+    args = ap.parse_args()
+
+    import torch
+
+    from self_play_reinforcement_learning_amd import distributed as D
+    from self_play_reinforcement_learning_amd.engine import SelfPlayEngine
+    from self_play_reinforcement_learning_amd.modules import ResidualTower
+
+    rank, world, local = D.init_from_env()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    torch.manual_seed(0)
+    net = ResidualTower(7, 6, 7, num_blocks=args.blocks, filter_factor=args.filter_factor).to(dev).eval()
+    eng = SelfPlayEngine("connect4", net, n_games=args.games, iterations=args.sims, seed=1234 + rank,
+                         device=dev, bucket=args.bucket)
+    gathered = []
+
+    def on_moves(m):
+        if not args.no_gather and D.is_distributed():
+            g = D.gather_moves(m, 42, 7)
+            if g is not None:
+                gathered.append(g["z"].shape[0])
+        else:
+            gathered.append(int(m["z"].shape[0]))
+
+    def one_step():
+        eng.ply(on_moves=on_moves if not args.no_gather else None)
+        D.all_reduce_stats(eng.stats_vector())  # episode-end statistics exchange
+
+    for _ in range(args.warmup):
+        one_step()
+    eng.check()
+    c0 = eng.counters()
+    eng.enable_timers(True)
+    rows0, pad0 = eng.nn_rows, eng.nn_rows_padded
+
+    D.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step()
+    D.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    elapsed_max = D.all_reduce_max(elapsed)
+
+    c1 = eng.counters()
+    eng.check()
+    moves_local = c1["moves"] - c0["moves"]
+    tot = D.all_reduce_stats([moves_local, c1["sims"] - c0["sims"], c1["games_finished"] - c0["games_finished"]])
+    moves_all, sims_all, games_all = (int(x) for x in tot)
+
+    # ---- select-kernel roofline (HIP events around k_select on the arena's stream)
+    sel_ms = eng.select_timer.total_ms()
+    sel_launches = eng.select_timer.count()
+    sims_local = c1["sims"] - c0["sims"]
+    levels_local = c1["depth_sum"] - c0["depth_sum"]
+    sel_bytes = select_bytes(sims_local, levels_local)
+    sel_avg_s = sel_ms / 1e3 / max(1, sel_launches)
+    bytes_per_launch = sel_bytes / max(1, sel_launches)
+    achieved = bytes_per_launch / sel_avg_s / 1e9 if sel_avg_s > 0 else 0.0
+
+    # ---- network (MFMA) share
+    nn_ms = eng.nn_timer.total_ms()
+    rows = eng.nn_rows - rows0
+    rows_padded = eng.nn_rows_padded - pad0
+    fpl = resnet_flops_per_leaf(7, 6, 7, args.filter_factor, args.blocks)
+    nn_tflops = rows * fpl / (nn_ms / 1e3) / 1e12 if nn_ms > 0 else 0.0
+
+    out = {
+        "metric": "self-play positions/sec (Connect4, 200 sims/move)",
+        "value": moves_all / elapsed_max,
+        "unit": "positions/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed_max / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (self-generated games, random-init ResNet weights, torch.manual_seed(0))",
+        "config": {
+            "workload": f"connect4 7x6 self-play, {args.sims} sims/move, {args.games} concurrent games per GPU "
+                        f"(2 trees each), ResNet-{4 * args.filter_factor}x{args.blocks} bf16 leaf eval, fp64 tree stats",
+            "games_per_gpu": args.games,
+            "global_games": args.games * world,
+            "sims_per_move": args.sims,
+            "net": f"ResidualTower(filter_factor={args.filter_factor}, num_blocks={args.blocks})",
+            "parallelism": f"dp{world}",
+        },
+        "roofline": {
+            "kernel": "k_select<C4> (PUCT tree walk)",
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "bytes_per_launch": bytes_per_launch,
+            "avg_launch_us": sel_avg_s * 1e6,
+            "launches": sel_launches,
+        },
+        "nn": {
+            "bound": "mfma",
+            "achieved_tflops": nn_tflops,
+            "peak_tflops": BF16_DENSE_PEAK_TFLOPS,
+            "frac": nn_tflops / BF16_DENSE_PEAK_TFLOPS,
+            "flops_per_leaf": fpl,
+            "rows": rows,
+            "rows_padded": rows_padded,
+            "nn_ms": nn_ms,
+            "share_of_step": nn_ms / 1e3 / elapsed if elapsed else None,
+        },
+        "tree": {
+            "sims": sims_all,
+            "mean_select_levels": levels_local / max(1, sims_local),
+            "terminal_leaf_frac": (c1["terminal_leaves"] - c0["terminal_leaves"]) / max(1, sims_local),
+            "games_finished": games_all,
+            "select_ms_share": sel_ms / 1e3 / elapsed if elapsed else None,
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cores = min(16, os.cpu_count() or 1)
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, cores, args.sims, args.filter_factor, args.blocks)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if D.is_distributed():
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,216 @@
+/*
+ * spmcts.h — C ABI of the MI355X-native batched self-play MCTS arena.
+ *
+ * The arena replaces the per-process Python object tree of the reference
+ * (reubenvanammers/self_play_reinforcement_learning, games/algos/mcts.py) and
+ * the per-game episode loop that drives it (games/algos/selfplayworker.py
+ * SelfPlayer, fed by games/algos/self_play_parallel.py SelfPlayScheduler).
+ * Thousands of trees live in one device-resident struct-of-arrays node store;
+ * every entry point below launches HIP kernels for gfx950 on the caller's
+ * stream.  The reference is pure Python, so there is no C FFI to bind: the
+ * drop-in boundary is the reference's own Python policy API (MCTreeSearch /
+ * SelfPlayScheduler / Memory), re-implemented in
+ * self_play_reinforcement_learning_amd/ on top of these functions via ctypes.
+ * Each function cites the reference interface it replaces.
+ *
+ * Conventions
+ *   - All array arguments named *_dev are DEVICE pointers owned by the caller
+ *     (torch tensors); the arena owns only its node store and game state.
+ *   - `stream` is a hipStream_t (NULL = legacy default stream).  Calls are
+ *     stream-ordered; none synchronises unless stated ("(sync)").
+ *   - Return value: 0 on success, < 0 on error; spmcts_last_error() returns a
+ *     thread-local message.  Errors raised on the device (node-pool
+ *     exhaustion, RNG tape exhaustion, invalid action) are sticky flags read by
+ *     spmcts_check() / spmcts_get_counters().
+ *   - No exceptions cross the ABI.  One arena per device per process; calls on
+ *     one arena must be serialised by the host (single writer).
+ *
+ * Board frame: +1 = the tree's owner (each MCTreeSearch sees itself as +1,
+ * selfplayworker.py:175-176).  Boards are int8/int64 [W][H] = [column][row],
+ * row 0 = bottom (connect4env.py:22).
+ */
+#ifndef SPMCTS_H
+#define SPMCTS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct spmcts_arena spmcts_arena; /* opaque */
+typedef void *spmcts_stream;              /* hipStream_t */
+
+enum spmcts_game { SPMCTS_CONNECT4 = 0, SPMCTS_TICTACTOE = 1 };
+enum spmcts_rng_mode {
+  SPMCTS_RNG_PHILOX = 0, /* rocRAND Philox4x32-10, one subsequence per tree          */
+  SPMCTS_RNG_TAPE = 1    /* replay injected per-tree double streams (parity mode)     */
+};
+enum spmcts_leaf_format {
+  SPMCTS_LEAF_F32 = 0,      /* float  planes [B,3,W,H] (empty, own, enemy)  modules.py:115-125 */
+  SPMCTS_LEAF_F16 = 1,      /* half   planes                                                   */
+  SPMCTS_LEAF_BF16 = 2,     /* bf16   planes                                                   */
+  SPMCTS_LEAF_BOARD_I64 = 3 /* int64 boards [B,W,H] = state * mover, for net.forward(s)        */
+};
+enum spmcts_layout { SPMCTS_NCHW = 0, SPMCTS_NHWC = 1 };
+
+/* device error flags (sticky) */
+#define SPMCTS_ERR_POOL 0x1u      /* a tree ran out of node blocks                 */
+#define SPMCTS_ERR_TAPE 0x2u      /* RNG tape exhausted                            */
+#define SPMCTS_ERR_NOCHILD 0x4u   /* select reached a node whose children are all invalid */
+#define SPMCTS_ERR_ACTION 0x8u    /* play_action on an illegal action              */
+#define SPMCTS_ERR_STATE 0x10u    /* inconsistent tree state                       */
+#define SPMCTS_ERR_EXPORT 0x20u   /* move export ring overflow                     */
+
+typedef struct spmcts_config {
+  int32_t game;            /* enum spmcts_game                                               */
+  int32_t width, height;   /* 7x6 Connect4, 3x3 TicTacToe (only these are instantiated)      */
+  int32_t n_trees;         /* tree slots (games mode needs >= 2*n_games)                     */
+  int32_t n_games;         /* game slots for the self-play state machine (0 = tree mode only) */
+  int32_t iterations;      /* simulations per move (mcts.py:125, sizes the node pool)        */
+  int32_t blocks_per_tree; /* node blocks per tree; 0 = worst case from iterations          */
+  int32_t rng_mode;        /* enum spmcts_rng_mode                                            */
+  int32_t strong_play;     /* mcts.py:133, :307-311                                           */
+  int32_t evaluate;        /* mcts.py:273-274 (temp / 20)                                     */
+  int32_t leaf_format;     /* enum spmcts_leaf_format                                         */
+  int32_t leaf_layout;     /* enum spmcts_layout (planes only)                                */
+  int32_t compact;         /* 1: leaf rows compacted in tree order; 0: one row per active slot */
+  int32_t reserved0;
+  double cpuct;            /* MCNode.cpuct = 4 (mcts.py:25)                                   */
+  double x_noise;          /* MCNode.x = 0.25 (mcts.py:25)                                    */
+  double alpha;            /* Dirichlet alpha (mcts.py:135)                                   */
+  uint64_t seed;           /* Philox key                                                      */
+  uint64_t subsequence0;   /* Philox subsequence of tree 0 (rank * n_trees for multi-GPU)     */
+} spmcts_config;
+
+typedef struct spmcts_counters {
+  int64_t sims;                /* simulations completed (search_node calls)                  */
+  int64_t nn_leaves;           /* leaves sent to the network (search + play_action)          */
+  int64_t terminal_leaves;     /* simulations that ended on a terminal leaf (no NN)          */
+  int64_t depth_sum;           /* sum over sims of edges descended (select depth D)          */
+  int64_t set_node_expansions; /* play_action expansions (mcts.py:203-208)                   */
+  int64_t moves;               /* moves played by searching trees (= Move records)           */
+  int64_t games_finished;
+  int64_t positions_exported;  /* Move records exported                                      */
+  int64_t results[2][3];       /* [swap_sides][win, draw, loss] (self_play_parallel.py:302-327) */
+  int64_t blocks_in_use_max;   /* peak node blocks used by any tree                          */
+  uint32_t error_flags;
+  uint32_t reserved;
+} spmcts_counters;
+
+/* ---- library ------------------------------------------------------------ */
+int spmcts_version(void);
+const char *spmcts_last_error(void);
+/* (sync) size of the device allocation an arena with this config needs */
+int spmcts_arena_bytes(const spmcts_config *cfg, uint64_t *bytes_out);
+
+/* ---- arena lifetime ------------------------------------------------------ */
+/* Replaces MCTreeSearch.__init__ (mcts.py:119-164) for many trees at once. */
+int spmcts_arena_create(const spmcts_config *cfg, int device, spmcts_arena **out);
+int spmcts_arena_destroy(spmcts_arena *h);
+/* geometry: A = actions, W, H, blocks per tree, lanes per tree */
+int spmcts_arena_geometry(const spmcts_arena *h, int32_t *A, int32_t *W, int32_t *H, int32_t *blocks_per_tree,
+                          int32_t *n_trees, int32_t *n_games);
+
+/* Priors of the empty-board root: `self.network(base_state)` in MCTreeSearch.reset
+ * (mcts.py:167-170).  Constant per network weights; used by every tree/game reset. */
+int spmcts_set_root_prior(spmcts_arena *h, const float *probs_dev /*[A]*/, spmcts_stream stream);
+/* Parity mode: per-tree flat double streams, consumed in the reference's call
+ * order (dirichlet(A) per search, rand(A) per select level, one uniform per
+ * np.random.choice).  offsets_dev[T+1] (int64) index into tape_dev. */
+int spmcts_set_tape(spmcts_arena *h, const double *tape_dev, const int64_t *offsets_dev, spmcts_stream stream);
+
+/* ---- tree-level API (the MCTreeSearch policy protocol) -------------------- */
+/* MCTreeSearch.reset(player) (mcts.py:166-174): new root on the empty board.
+ * priors_dev: NULL = the arena's root prior, else [n][A] per tree. */
+int spmcts_tree_reset(spmcts_arena *h, const int32_t *trees_dev, const int8_t *root_player_dev,
+                      const float *priors_dev, int32_t n, spmcts_stream stream);
+/* MCTreeSearch.search prologue (mcts.py:323-327): Dirichlet noise on the roots of
+ * the listed trees; they become the active set for spmcts_select. */
+int spmcts_search_begin(spmcts_arena *h, const int32_t *trees_dev, int32_t n, spmcts_stream stream);
+/* One search_node (mcts.py:340-367) for every active tree: PUCT select with
+ * jitter, terminal leaves backed up in place, other leaves written to the leaf
+ * batch (rows in tree order).  *leaf_count_dev = rows written. */
+int spmcts_select(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_dev, spmcts_stream stream);
+/* spmcts_select in two launches (for per-kernel timing): the tree walk alone,
+ * then the leaf-row compaction + encode of whatever is pending. */
+int spmcts_select_tree(spmcts_arena *h, spmcts_stream stream);
+int spmcts_leaf_rows(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_dev, spmcts_stream stream);
+/* _expand_node tail + backup (mcts.py:316-321, :94-98, :361-364) for the rows of
+ * the last select / play_action: create children with the network's priors,
+ * back the value up the path.  probs_dev [rows][A] f32, values_dev [rows] f32
+ * (network outputs from the mover's perspective, modules.py:109-112). */
+int spmcts_expand(spmcts_arena *h, const float *probs_dev, const float *values_dev, spmcts_stream stream);
+/* MCTreeSearch._play (mcts.py:272-299) for the active trees + remove_noise:
+ * visit-count^(1/temp) distribution, np.random.choice semantics, Move record.
+ * Outputs per active tree i: actions_dev[i], states_dev[i][W*H] (int8, tree
+ * frame), tree_probs_dev[i][A], q_dev[i] (double; exported as a float32 tensor
+ * unless q_f64_dev[i]), recorded_dev[i] (0 = numpy ValueError fallback). */
+int spmcts_search_end(spmcts_arena *h, double temp, int32_t *actions_dev, int8_t *states_dev, float *tree_probs_dev,
+                      double *q_dev, uint8_t *q_f64_dev, uint8_t *recorded_dev, spmcts_stream stream);
+/* MCTreeSearch.play_action/_set_node (mcts.py:188-209): advance each listed
+ * root; an unvisited child is expanded (rows for the network) and backed up. */
+int spmcts_play_action(spmcts_arena *h, const int32_t *trees_dev, const int32_t *actions_dev, int32_t n,
+                       void *leaves_dev, int32_t *leaf_count_dev, spmcts_stream stream);
+/* Tree id of every leaf row of the last select / play_action / games_end_ply
+ * (rows in tree order; trees_dev has room for n_trees entries). */
+int spmcts_leaf_trees(spmcts_arena *h, int32_t *trees_dev, spmcts_stream stream);
+/* (sync) root statistics of one tree: children n/w/p (A each), root n/w, player, board */
+int spmcts_root_stats(spmcts_arena *h, int32_t tree, int32_t *child_n, double *child_w, float *child_p,
+                      int32_t *root_n, double *root_w, int32_t *root_player, int8_t *board /*[W*H]*/);
+
+/* ---- games-level API (SelfPlayer.play_episode state machine) -------------- */
+/* Start games in the listed slots (selfplayworker.py:172-179): both trees reset,
+ * swap_sides = game id odd (self_play_parallel.py:237).  Game ids continue from
+ * the arena's counter. */
+int spmcts_games_start(spmcts_arena *h, const int32_t *slots_dev, const float *priors_dev /* NULL or [n][2][A] */,
+                       int32_t n, spmcts_stream stream);
+/* Cap on games started by automatic refill (< 0 = unlimited). */
+int spmcts_games_set_limit(spmcts_arena *h, int64_t max_games);
+/* Each active game's player to move begins its search (noise); active set = movers. */
+int spmcts_games_begin_ply(spmcts_arena *h, spmcts_stream stream);
+/* Each active game: _play on the mover, Move recorded, env.step, play_action on
+ * both trees (selfplayworker.py:209-224); expansions go to the leaf batch. */
+int spmcts_games_end_ply(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_dev, spmcts_stream stream);
+/* Finished games: result, push_to_queue of both trees' Moves into the export
+ * ring (mcts.py:225-232, selfplayworker.py:185-190), refill (if `refill`).
+ * out_dev[0] = games finished this ply, out_dev[1] = records in the ring. */
+int spmcts_games_finish_ply(spmcts_arena *h, int32_t refill, int32_t *out_dev /*[2]*/, spmcts_stream stream);
+/* Copy the export ring out and clear it: states int8 [n][W*H], tree_probs f32
+ * [n][A], q f64 [n], q_f64 u8 [n], z f32 [n] (actual_val), game ids i64 [n]. */
+int spmcts_export_moves(spmcts_arena *h, int8_t *states_dev, float *tree_probs_dev, double *q_dev, uint8_t *q_f64_dev,
+                        float *z_dev, int64_t *game_dev, int32_t max_records, int32_t *count_dev,
+                        spmcts_stream stream);
+/* (sync) per-slot game state: active flag, ply, swap, game id */
+int spmcts_games_state(spmcts_arena *h, uint8_t *active, int32_t *ply, uint8_t *swap, int64_t *game_id);
+
+/* ---- diagnostics --------------------------------------------------------- */
+int spmcts_get_counters(spmcts_arena *h, spmcts_counters *out); /* (sync) */
+int spmcts_check(spmcts_arena *h);                                /* (sync) <0 if a device error flag is set */
+
+/* ---- stand-alone kernels -------------------------------------------------- */
+/* Batched env step (Connect4Env.step connect4env.py:29-43 / TicTacToeEnv.step
+ * tictactoe_env.py:23-33) on device: boards int8 [n][W][H]. status: 0 ok,
+ * 1 ValueError (full column), 2 GameOver (over_dev[i] set). */
+int spmcts_env_step(int32_t game, int32_t width, int32_t height, const int8_t *boards_dev, const int32_t *actions_dev,
+                    const int8_t *players_dev, const uint8_t *over_dev, int32_t n, int8_t *out_boards_dev,
+                    int8_t *reward_dev, uint8_t *done_dev, int8_t *status_dev, uint8_t *valid_dev,
+                    spmcts_stream stream);
+/* Host-compiled twin of the same bitboard code (single board, host pointers), used
+ * by the Python env facade for interactive play (not on the self-play path). */
+int spmcts_env_step_host(int32_t game, int32_t width, int32_t height, int8_t *board /*[W][H] in/out*/,
+                         int32_t action, int32_t player, int32_t *reward, int32_t *done);
+int spmcts_valid_moves_host(int32_t game, int32_t width, int32_t height, const int8_t *board, uint8_t *valid);
+/* Deterministic table network (oracle/table_net.py) over leaf rows, for bit-exact
+ * search parity tests: leaves in any spmcts_leaf_format/layout; per-row salts optional. */
+int spmcts_table_net(int32_t game, int32_t width, int32_t height, const void *leaves_dev, int32_t leaf_format,
+                     int32_t leaf_layout, int32_t n, uint64_t salt, const uint64_t *salts_dev /* [n] or NULL */,
+                     float *probs_dev, float *values_dev, spmcts_stream stream);
+/* Memory-roofline helper: device copy bandwidth probe (bytes each way). */
+int spmcts_copy_probe(const void *src_dev, void *dst_dev, uint64_t bytes, spmcts_stream stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPMCTS_H */

@@ -1,0 +1,303 @@
+"""Python handle on one device arena (include/spmcts.h) — torch tensors in, torch tensors out.
+
+All buffers handed to the library are torch tensors on the arena's device; the
+library launches on `torch.cuda.current_stream()` of that device, so the
+network that consumes the leaf rows runs on the same stream with no extra
+synchronisation.  The only host round trip per simulation is reading the
+number of leaf rows (`select()` returns it as a Python int).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call, ptr
+
+GAMES = {"connect4": (_lib.CONNECT4, 7, 6, 7), "tictactoe": (_lib.TICTACTOE, 3, 3, 9)}
+LEAF_FORMATS = {"f32": _lib.LEAF_F32, "f16": _lib.LEAF_F16, "bf16": _lib.LEAF_BF16, "board": _lib.LEAF_BOARD_I64}
+_LEAF_DTYPES = {"f32": torch.float32, "f16": torch.float16, "bf16": torch.bfloat16, "board": torch.int64}
+
+
+def game_of_env(env):
+    """Map a reference-style env (class or instance) to an arena game name.
+
+    Accepts this package's envs and the reference's Connect4Env / TicTacToeEnv
+    (games/connect4/connect4env.py, games/tictactoe/tictactoe_env.py) by shape.
+    """
+    e = env() if isinstance(env, type) else env
+    name = type(e).__name__.lower()
+    w, h = getattr(e, "width", None), getattr(e, "height", None)
+    n = e.action_space.n if hasattr(e, "action_space") else getattr(e, "n_actions", None)
+    if "connect4" in name or (w, h, n) == (7, 6, 7):
+        game = "connect4"
+    elif "tictactoe" in name or (w, h, n) == (3, 3, 9):
+        game = "tictactoe"
+    else:
+        raise ValueError(f"unsupported environment {type(e).__name__}")
+    gid, W, H, A = GAMES[game]
+    if (w, h) != (W, H):
+        raise ValueError(f"{game} arena is instantiated for {W}x{H} boards only, got {w}x{h}")
+    return game
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class Arena:
+    """A device-resident forest of MCTS trees (+ optional self-play game slots)."""
+
+    def __init__(self, game="connect4", n_trees=2, n_games=0, iterations=100, rng="philox", seed=0,
+                 subsequence0=0, strong_play=False, evaluate=False, leaf_format="bf16", leaf_layout="nchw",
+                 cpuct=4.0, x_noise=0.25, alpha=1.0, blocks_per_tree=0, device=None):
+        if not torch.cuda.is_available():
+            raise _lib.SpmctsError("the HIP arena needs a GPU (torch.cuda.is_available() is False)")
+        gid, W, H, A = GAMES[game]
+        self.game, self.W, self.H, self.A = game, W, H, A
+        self.cells = W * H
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else
+                                   torch.device(device).index or 0)
+        self.n_trees, self.n_games = n_trees, n_games
+        self.leaf_format, self.leaf_layout = leaf_format, leaf_layout
+        cfg = _lib.Config()
+        cfg.game, cfg.width, cfg.height = gid, W, H
+        cfg.n_trees, cfg.n_games, cfg.iterations = n_trees, n_games, iterations
+        cfg.blocks_per_tree = blocks_per_tree
+        cfg.rng_mode = _lib.RNG_TAPE if rng == "tape" else _lib.RNG_PHILOX
+        cfg.strong_play, cfg.evaluate = int(bool(strong_play)), int(bool(evaluate))
+        cfg.leaf_format = LEAF_FORMATS[leaf_format]
+        cfg.leaf_layout = _lib.NHWC if leaf_layout == "nhwc" else _lib.NCHW
+        cfg.compact = 1
+        cfg.cpuct, cfg.x_noise, cfg.alpha = float(cpuct), float(x_noise), float(alpha)
+        cfg.seed, cfg.subsequence0 = int(seed) & (2**64 - 1), int(subsequence0)
+        self.cfg = cfg
+        L = _lib.lib()
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            call("spmcts_arena_create", ctypes.byref(cfg), self.device.index, ctypes.byref(h))
+        self.h = h
+        geo = [ctypes.c_int32() for _ in range(6)]
+        call("spmcts_arena_geometry", h, *[ctypes.byref(g) for g in geo])
+        self.blocks_per_tree = geo[3].value
+        dev = self.device
+        rows = max(n_trees, n_games, 1)
+        self.max_rows = rows
+        if leaf_format == "board":
+            self._leaves = torch.zeros((rows, W, H), dtype=torch.int64, device=dev)
+        elif leaf_layout == "nhwc":
+            self._leaves = torch.zeros((rows, W, H, 3), dtype=_LEAF_DTYPES[leaf_format], device=dev)
+        else:
+            self._leaves = torch.zeros((rows, 3, W, H), dtype=_LEAF_DTYPES[leaf_format], device=dev)
+        self._count = torch.zeros(4, dtype=torch.int32, device=dev)
+        self._count_host = torch.zeros(4, dtype=torch.int32).pin_memory()
+        self._finish = torch.zeros(2, dtype=torch.int32, device=dev)
+        self._i32 = torch.zeros(rows, dtype=torch.int32, device=dev)
+        self._i8 = torch.zeros(rows, dtype=torch.int8, device=dev)
+        self.n_active = 0
+        self._L = L
+
+    # ------------------------------------------------------------------ lifetime
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            _lib.lib().spmcts_arena_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ helpers
+    def _dev_i32(self, xs):
+        return torch.as_tensor(np.asarray(xs, dtype=np.int32)).to(self.device)
+
+    def _dev_i8(self, xs):
+        return torch.as_tensor(np.asarray(xs, dtype=np.int8)).to(self.device)
+
+    def leaves(self, n):
+        """Leaf rows [:n] as the network's input tensor ([n, 3, W, H]; channels_last if NHWC)."""
+        x = self._leaves[:n]
+        if self.leaf_format != "board" and self.leaf_layout == "nhwc":
+            x = x.permute(0, 3, 1, 2)  # NCHW view with channels_last strides
+        return x
+
+    def _read_count(self):
+        self._count_host.copy_(self._count, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        return int(self._count_host[0])
+
+    # ------------------------------------------------------------------ configuration
+    def set_root_prior(self, probs):
+        p = torch.as_tensor(probs, dtype=torch.float32).to(self.device).contiguous()
+        self._root_prior = p
+        call("spmcts_set_root_prior", self.h, ptr(p), _stream())
+
+    def set_tapes(self, tapes):
+        """Parity mode: one flat float64 stream per tree (list indexed by tree id)."""
+        offs = np.zeros(self.n_trees + 1, dtype=np.int64)
+        for t in range(self.n_trees):
+            offs[t + 1] = offs[t] + (len(tapes[t]) if t < len(tapes) and tapes[t] is not None else 0)
+        flat = np.concatenate([np.asarray(tapes[t], dtype=np.float64) for t in range(min(len(tapes), self.n_trees))
+                               if tapes[t] is not None] + [np.zeros(1)])
+        self._tape = torch.as_tensor(flat).to(self.device)
+        self._tape_offs = torch.as_tensor(offs).to(self.device)
+        call("spmcts_set_tape", self.h, ptr(self._tape), ptr(self._tape_offs), _stream())
+
+    # ------------------------------------------------------------------ tree API
+    def tree_reset(self, trees, players, priors=None):
+        """priors: optional float32 [n, A] per-tree root priors (default: the arena's root prior)."""
+        t = self._dev_i32(trees)
+        p = self._dev_i8(players)
+        pr = None if priors is None else torch.as_tensor(priors, dtype=torch.float32).to(self.device).contiguous()
+        call("spmcts_tree_reset", self.h, ptr(t), ptr(p), ptr(pr), len(trees), _stream())
+
+    def search_begin(self, trees):
+        t = self._dev_i32(trees)
+        self._active = t
+        self.n_active = len(trees)
+        call("spmcts_search_begin", self.h, ptr(t), len(trees), _stream())
+
+    def select(self, timer=None):
+        """One simulation for every active tree; returns the number of leaf rows to evaluate.
+
+        `timer` (optional): object with start()/stop() bracketing the tree-walk kernel alone
+        (HIP events on this stream, used by bench.py for the select roofline)."""
+        if timer is None:
+            call("spmcts_select", self.h, ptr(self._leaves), ptr(self._count), _stream())
+        else:
+            timer.start()
+            call("spmcts_select_tree", self.h, _stream())
+            timer.stop()
+            call("spmcts_leaf_rows", self.h, ptr(self._leaves), ptr(self._count), _stream())
+        return self._read_count()
+
+    def expand(self, probs, values):
+        probs = probs.float().contiguous()
+        values = values.float().reshape(-1).contiguous()
+        call("spmcts_expand", self.h, ptr(probs), ptr(values), _stream())
+
+    def search_end(self, temp=1.0):
+        n = self.n_active
+        dev = self.device
+        out = dict(
+            action=torch.zeros(n, dtype=torch.int32, device=dev),
+            state=torch.zeros((n, self.cells), dtype=torch.int8, device=dev),
+            tree_probs=torch.zeros((n, self.A), dtype=torch.float32, device=dev),
+            q=torch.zeros(n, dtype=torch.float64, device=dev),
+            q_f64=torch.zeros(n, dtype=torch.uint8, device=dev),
+            recorded=torch.zeros(n, dtype=torch.uint8, device=dev),
+        )
+        call("spmcts_search_end", self.h, float(temp), ptr(out["action"]), ptr(out["state"]), ptr(out["tree_probs"]),
+             ptr(out["q"]), ptr(out["q_f64"]), ptr(out["recorded"]), _stream())
+        return out
+
+    def play_action(self, trees, actions):
+        t = self._dev_i32(trees)
+        a = self._dev_i32(actions)
+        call("spmcts_play_action", self.h, ptr(t), ptr(a), len(trees), ptr(self._leaves), ptr(self._count), _stream())
+        return self._read_count()
+
+    def leaf_trees(self, n):
+        """Tree id of each of the first n leaf rows (device int32 tensor)."""
+        out = torch.empty(self.n_trees, dtype=torch.int32, device=self.device)
+        call("spmcts_leaf_trees", self.h, ptr(out), _stream())
+        return out[:n]
+
+    def root_stats(self, tree):
+        A, cells = self.A, self.cells
+        cn = (ctypes.c_int32 * A)()
+        cw = (ctypes.c_double * A)()
+        cp = (ctypes.c_float * A)()
+        rn, rw, rp = ctypes.c_int32(), ctypes.c_double(), ctypes.c_int32()
+        board = (ctypes.c_int8 * cells)()
+        torch.cuda.current_stream().synchronize()
+        call("spmcts_root_stats", self.h, int(tree), cn, cw, cp, ctypes.byref(rn), ctypes.byref(rw), ctypes.byref(rp),
+             board)
+        return dict(child_n=list(cn), child_w=list(cw), child_p=list(cp), root_n=rn.value, root_w=rw.value,
+                    root_player=rp.value, board=np.array(list(board), dtype=np.int8).reshape(self.W, self.H))
+
+    # ------------------------------------------------------------------ games API
+    def games_start(self, slots, priors=None):
+        """priors: optional float32 [n, 2, A] (policy tree, opponent tree) root priors per game."""
+        s = self._dev_i32(slots)
+        pr = None if priors is None else torch.as_tensor(priors, dtype=torch.float32).to(self.device).contiguous()
+        call("spmcts_games_start", self.h, ptr(s), ptr(pr), len(slots), _stream())
+
+    def games_set_limit(self, max_games):
+        torch.cuda.current_stream().synchronize()
+        call("spmcts_games_set_limit", self.h, int(max_games))
+
+    def games_begin_ply(self):
+        self.n_active = self.n_games
+        call("spmcts_games_begin_ply", self.h, _stream())
+
+    def games_end_ply(self):
+        call("spmcts_games_end_ply", self.h, ptr(self._leaves), ptr(self._count), _stream())
+        return self._read_count()
+
+    def games_finish_ply(self, refill=True):
+        call("spmcts_games_finish_ply", self.h, int(bool(refill)), ptr(self._finish), _stream())
+        f = self._finish.cpu()
+        return int(f[0]), int(f[1])
+
+    def export_moves(self, max_records):
+        dev = self.device
+        n = max(1, int(max_records))
+        out = dict(
+            state=torch.zeros((n, self.cells), dtype=torch.int8, device=dev),
+            tree_probs=torch.zeros((n, self.A), dtype=torch.float32, device=dev),
+            q=torch.zeros(n, dtype=torch.float64, device=dev),
+            q_f64=torch.zeros(n, dtype=torch.uint8, device=dev),
+            z=torch.zeros(n, dtype=torch.float32, device=dev),
+            game=torch.zeros(n, dtype=torch.int64, device=dev),
+        )
+        call("spmcts_export_moves", self.h, ptr(out["state"]), ptr(out["tree_probs"]), ptr(out["q"]),
+             ptr(out["q_f64"]), ptr(out["z"]), ptr(out["game"]), n, ptr(self._count), _stream())
+        k = self._read_count()
+        return {key: v[:k] for key, v in out.items()}
+
+    def games_state(self):
+        G = self.n_games
+        active = (ctypes.c_uint8 * G)()
+        ply = (ctypes.c_int32 * G)()
+        swap = (ctypes.c_uint8 * G)()
+        gid = (ctypes.c_int64 * G)()
+        torch.cuda.current_stream().synchronize()
+        call("spmcts_games_state", self.h, active, ply, swap, gid)
+        return dict(state=np.array(list(active)), ply=np.array(list(ply)), swap=np.array(list(swap)),
+                    game_id=np.array(list(gid)))
+
+    # ------------------------------------------------------------------ diagnostics
+    def counters(self):
+        c = _lib.Counters()
+        torch.cuda.current_stream().synchronize()
+        call("spmcts_get_counters", self.h, ctypes.byref(c))
+        return c.as_dict()
+
+    def check(self):
+        torch.cuda.current_stream().synchronize()
+        rc = _lib.lib().spmcts_check(self.h)
+        if rc != 0:
+            c = self.counters()
+            raise _lib.SpmctsError(f"arena device error: {_lib.describe_flags(c['error_flags'])}")
+
+
+def table_net_eval(game, leaves, leaf_format, leaf_layout, salt=0, salts=None):
+    """Run the deterministic table network kernel over leaf rows (parity tests / smoke).
+
+    `salts` (int64 tensor [n] on the device, optional) gives every row its own network."""
+    gid, W, H, A = GAMES[game]
+    n = leaves.shape[0]
+    dev = leaves.device
+    probs = torch.empty((max(n, 1), A), dtype=torch.float32, device=dev)
+    values = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
+    if n:
+        src = leaves
+        if leaf_format != "board" and leaf_layout == "nhwc":
+            src = leaves.permute(0, 2, 3, 1)  # back to the NHWC storage order
+        call("spmcts_table_net", gid, W, H, ptr(src), LEAF_FORMATS[leaf_format],
+             _lib.NHWC if leaf_layout == "nhwc" else _lib.NCHW, n, int(salt) & (2**64 - 1),
+             ptr(salts) if salts is not None else None, ptr(probs), ptr(values), _stream())
+    return probs[:n], values[:n]

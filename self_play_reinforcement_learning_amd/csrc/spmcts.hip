@@ -1,0 +1,1644 @@
+// spmcts.hip — MI355X (gfx950) batched self-play MCTS arena: kernels + C ABI.
+//
+// Replaces the per-game Python object tree of games/algos/mcts.py (MCNode /
+// MCTreeSearch) and the episode loop of games/algos/selfplayworker.py
+// (SelfPlayer) with one device-resident arena:
+//
+//   node store   SoA, one "child block" per expansion: n[APAD] i32, w[APAD] f64,
+//                p[APAD] f32, child[APAD] i32 (local block of the child's own
+//                children, -1 = unexpanded), vmask u32 per block (valid children).
+//                A node = (block, slot); trees own disjoint block ranges.
+//   trees        root node, root board (2 x u64 bitboards), root player, bump
+//                allocator, Dirichlet noise, per-sim path scratch, RNG.
+//   games        SelfPlayer state machine: board (policy frame), ply, swap_sides,
+//                two trees, Move record buffers, export ring.
+//
+// Every simulation of every active tree runs in lock step:
+//   k_select   one APAD-lane group per tree walks root -> leaf, scoring the A
+//              children of each node lane-parallel in fp64 (bit-exact with the
+//              reference's Python float arithmetic: fp-contract off), argmax via
+//              in-group shuffles, jitter from Philox or the parity tape;
+//              terminal leaves are backed up in place (no network call).
+//   k_scan     orders pending leaves by tree id (deterministic rows).
+//   k_encode   writes network input rows (planes or boards) for those leaves.
+//   [network on the same stream — PyTorch ResNet or the table net]
+//   k_expand   creates the leaf's child block from the priors, backs the value up.
+//
+// Compile: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off (see Makefile).
+#include <hip/hip_runtime.h>
+#include <rocrand/rocrand_normal.h>
+#include <rocrand/rocrand_philox4x32_10.h>
+#include <rocrand/rocrand_uniform.h>
+
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "board.h"
+#include "spmcts.h"
+
+#pragma clang fp contract(off)
+
+using namespace spm;
+
+// ----------------------------------------------------------------------------
+// error reporting
+// ----------------------------------------------------------------------------
+static thread_local std::string g_last_error;
+
+static int fail(int code, const std::string &msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+  do {                                                                                         \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess)                                                                      \
+      return fail(-(int)_e - 1000, std::string(#expr) + ": " + hipGetErrorString(_e));        \
+  } while (0)
+
+#define LAUNCH_CHECK()                                                                         \
+  do {                                                                                         \
+    hipError_t _e = hipGetLastError();                                                         \
+    if (_e != hipSuccess) return fail(-(int)_e - 1000, std::string("launch: ") + hipGetErrorString(_e)); \
+  } while (0)
+
+// ----------------------------------------------------------------------------
+// device view of an arena (passed by value to kernels)
+// ----------------------------------------------------------------------------
+typedef rocrand_state_philox4x32_10 Philox;
+
+struct View {
+  int T, cap, G, A;
+  double cpuct, x, alpha;
+  int strong, evaluate, rng_mode, leaf_format, leaf_layout;
+  // node store
+  int32_t *bn;
+  double *bw;
+  float *bp;
+  int32_t *bc;
+  uint32_t *bvm;
+  uint8_t *bf64;  // "w is a numpy float64" (strong_play dtype quirk, mcts.py:287/:308)
+  // trees
+  int32_t *root;
+  uint64_t *rpos, *rneg;
+  int8_t *rplayer;
+  int32_t *used;
+  double *noise;
+  uint8_t *noise_on;
+  int32_t *pnode;   // [T][MAXD] path node ids (root .. parent of leaf)
+  int32_t *pn;      // [T][MAXD] their visit counts as read during select
+  double *pw;       // [T][MAXD] their w as read during select
+  int32_t *plen;
+  int32_t *leaf;    // leaf node (local id)
+  int32_t *leaf_n;
+  double *leaf_w;
+  uint64_t *lpos, *lneg;
+  int8_t *lmover;
+  uint8_t *need;
+  Philox *rng;
+  const double *tape;
+  const int64_t *tape_end;  // [T] end offset
+  int64_t *tape_cur;        // [T]
+  int64_t *cnt;             // per-tree counters [T][8]
+  int32_t *active;
+  int32_t *row_tree;
+  int32_t *row_count;
+  float *root_prior;
+  uint32_t *err;
+  // games
+  uint64_t *gpos, *gneg;
+  int32_t *gply;
+  uint8_t *gswap, *gstate;
+  int8_t *gresult;
+  int64_t *gid;
+  int8_t *mv_state;
+  float *mv_probs;
+  double *mv_q;
+  uint8_t *mv_qf64;
+  int32_t *mv_count;
+  int8_t *ex_state;
+  float *ex_probs;
+  double *ex_q;
+  uint8_t *ex_qf64;
+  float *ex_z;
+  int64_t *ex_game;
+  int32_t *ex_count;
+  int32_t ex_cap;
+  int64_t *gcnt;  // games counters: [0] finished [1..6] results [7] next id [8] limit [9] exported
+  int32_t *gscratch;
+};
+
+enum { C_SIMS = 0, C_NN = 1, C_TERM = 2, C_DEPTH = 3, C_SETNODE = 4, C_MOVES = 5, C_NCNT = 8 };
+enum { GS_IDLE = 0, GS_ACTIVE = 1, GS_DONE = 2 };
+
+__device__ __forceinline__ void set_err(const View &v, uint32_t f) { atomicOr(v.err, f); }
+
+template <class G>
+__device__ __forceinline__ size_t nbase(const View &v, int tree) {
+  return (size_t)tree * (size_t)v.cap * G::APAD;
+}
+
+// ----------------------------------------------------------------------------
+// RNG: Philox (rocRAND) or parity tape
+// ----------------------------------------------------------------------------
+struct TreeRng {
+  Philox st;
+  int64_t cur, end;
+};
+
+__device__ __forceinline__ void rng_load(const View &v, int tree, TreeRng &r) {
+  if (v.rng_mode == SPMCTS_RNG_TAPE) {
+    r.cur = v.tape_cur[tree];
+    r.end = v.tape_end[tree];
+  } else {
+    r.st = v.rng[tree];
+  }
+}
+
+__device__ __forceinline__ void rng_store(const View &v, int tree, const TreeRng &r) {
+  if (v.rng_mode == SPMCTS_RNG_TAPE)
+    v.tape_cur[tree] = r.cur;
+  else
+    v.rng[tree] = r.st;
+}
+
+// One double in [0, 1) for lane `j` of a k-wide vector draw (all lanes call it with the
+// same state; the shared state then advances by k via rng_advance).
+__device__ __forceinline__ double rng_lane(const View &v, const TreeRng &r, int j, bool *tape_err) {
+  if (v.rng_mode == SPMCTS_RNG_TAPE) {
+    const int64_t i = r.cur + j;
+    if (i >= r.end) {
+      *tape_err = true;
+      return 0.0;
+    }
+    return v.tape[i];
+  }
+  Philox s = r.st;
+  skipahead(2ull * (unsigned long long)j, &s);
+  return 1.0 - rocrand_uniform_double(&s);  // rocRAND gives (0, 1]
+}
+
+__device__ __forceinline__ void rng_advance(const View &v, TreeRng &r, int k) {
+  if (v.rng_mode == SPMCTS_RNG_TAPE)
+    r.cur += k;
+  else
+    skipahead(2ull * (unsigned long long)k, &r.st);
+}
+
+// sequential scalar draw (single thread)
+__device__ __forceinline__ double rng_next(const View &v, TreeRng &r, bool *tape_err) {
+  double u = rng_lane(v, r, 0, tape_err);
+  rng_advance(v, r, 1);
+  return u;
+}
+
+// Gamma(alpha, 1): alpha == 1 -> Exp(1) = -log U; otherwise Marsaglia-Tsang.
+__device__ double gamma_draw(Philox *s, double alpha) {
+  if (alpha == 1.0) return -log(rocrand_uniform_double(s));
+  double boost = 1.0;
+  if (alpha < 1.0) {
+    boost = pow(rocrand_uniform_double(s), 1.0 / alpha);
+    alpha += 1.0;
+  }
+  const double d = alpha - 1.0 / 3.0, c = 1.0 / sqrt(9.0 * d);
+  for (int it = 0; it < 256; ++it) {
+    const double xn = rocrand_normal_double(s);
+    double t = 1.0 + c * xn;
+    if (t <= 0.0) continue;
+    t = t * t * t;
+    const double u = rocrand_uniform_double(s);
+    if (log(u) < 0.5 * xn * xn + d - d * t + d * log(t)) return d * t * boost;
+  }
+  return d * boost;
+}
+
+// ----------------------------------------------------------------------------
+// small helpers
+// ----------------------------------------------------------------------------
+template <class G>
+__device__ __forceinline__ void reset_tree(const View &v, int tree, int player, const float *prior) {
+  constexpr int P = G::APAD;
+  const size_t nb = nbase<G>(v, tree);
+  const size_t bb = (size_t)tree * v.cap;
+  // block 0 = pseudo block holding the root in slot 0; block 1 = root's children
+  v.bn[nb + 0] = 0;
+  v.bw[nb + 0] = 0.0;
+  v.bp[nb + 0] = 0.f;
+  v.bc[nb + 0] = 1;
+  v.bf64[nb + 0] = 0;
+  for (int j = 0; j < P; ++j) {
+    v.bn[nb + P + j] = 0;
+    v.bw[nb + P + j] = 0.0;
+    v.bp[nb + P + j] = j < G::A ? prior[j] : 0.f;
+    v.bc[nb + P + j] = -1;
+    v.bf64[nb + P + j] = 0;
+  }
+  v.bvm[bb + 0] = 1u;
+  v.bvm[bb + 1] = legal_mask<G>(Board{0, 0});
+  v.used[tree] = 2;
+  v.root[tree] = 0;
+  v.rpos[tree] = 0;
+  v.rneg[tree] = 0;
+  v.rplayer[tree] = (int8_t)player;
+  v.noise_on[tree] = 0;
+  v.need[tree] = 0;
+}
+
+// terminal value of _expand_node (mcts.py:305-313); r = reward * mover
+__device__ __forceinline__ double terminal_value(const View &v, Board parent, int r) {
+  if (v.strong) {
+    const int num_steps = popc(parent.pos | parent.neg) + 1;  // np.sum(np.abs(state)) + 1
+    return (1.18 - ((double)(9 * num_steps) / 350.0)) * (double)r;
+  }
+  return (double)r;
+}
+
+// Dirichlet root noise (add_noise, mcts.py:49-53): A components, invalid children included.
+template <class G>
+__device__ void draw_noise(const View &v, int tree) {
+  TreeRng r;
+  rng_load(v, tree, r);
+  double g[G::A];
+  if (v.rng_mode == SPMCTS_RNG_TAPE) {
+    bool terr = false;
+    for (int j = 0; j < G::A; ++j) g[j] = rng_lane(v, r, j, &terr);
+    rng_advance(v, r, G::A);
+    if (terr) set_err(v, SPMCTS_ERR_TAPE);
+  } else {
+    double acc = 0.0;
+    for (int j = 0; j < G::A; ++j) {
+      g[j] = gamma_draw(&r.st, v.alpha);
+      acc += g[j];
+    }
+    const double inv = acc > 0.0 ? 1.0 / acc : 0.0;
+    for (int j = 0; j < G::A; ++j) g[j] *= inv;
+  }
+  for (int j = 0; j < G::A; ++j) v.noise[(size_t)tree * G::APAD + j] = g[j];
+  v.noise_on[tree] = 1;
+  rng_store(v, tree, r);
+}
+
+// ----------------------------------------------------------------------------
+// kernels: resets / noise
+// ----------------------------------------------------------------------------
+template <class G>
+__global__ void k_tree_reset(View v, const int32_t *trees, const int8_t *players, const float *priors, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int t = trees[i];
+  if (t < 0 || t >= v.T) {
+    set_err(v, SPMCTS_ERR_STATE);
+    return;
+  }
+  reset_tree<G>(v, t, players[i], priors ? priors + (size_t)i * G::A : v.root_prior);
+}
+
+template <class G>
+__global__ void k_search_begin(View v, const int32_t *trees, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int t = trees[i];
+  v.active[i] = t;
+  if (t < 0) return;
+  draw_noise<G>(v, t);
+}
+
+// ----------------------------------------------------------------------------
+// kernel: select (search_node, mcts.py:340-367)
+// ----------------------------------------------------------------------------
+template <int P>
+__device__ __forceinline__ void group_argmax(double &s, int &idx) {
+#pragma unroll
+  for (int off = P / 2; off > 0; off >>= 1) {
+    const double so = __shfl_xor(s, off, P);
+    const int io = __shfl_xor(idx, off, P);
+    if (so > s || (so == s && io < idx)) {
+      s = so;
+      idx = io;
+    }
+  }
+}
+
+template <int P>
+__device__ __forceinline__ int group_or(int x) {
+#pragma unroll
+  for (int off = P / 2; off > 0; off >>= 1) x |= __shfl_xor(x, off, P);
+  return x;
+}
+
+template <class G>
+__global__ __launch_bounds__(64) void k_select(View v, int n_active) {
+  constexpr int P = G::APAD;
+  constexpr int GPB = 64 / P;  // groups (trees) per block
+  __shared__ int32_t s_node[GPB][G::MAXD];
+  __shared__ int32_t s_n[GPB][G::MAXD];
+  __shared__ double s_w[GPB][G::MAXD];
+
+  const int lane = threadIdx.x & (P - 1);
+  const int grp = threadIdx.x / P;
+  const int slot = blockIdx.x * GPB + grp;
+  if (slot >= n_active) return;
+  const int tree = v.active[slot];
+  if (tree < 0) return;
+
+  const size_t nb = nbase<G>(v, tree);
+  const size_t bb = (size_t)tree * v.cap;
+  int node = v.root[tree];
+  Board b{v.rpos[tree], v.rneg[tree]};
+  int player = v.rplayer[tree];
+  const bool noise = v.noise_on[tree] != 0;
+  const double nz = (noise && lane < G::A) ? v.noise[(size_t)tree * P + lane] : 0.0;
+  TreeRng rng;
+  rng_load(v, tree, rng);
+  bool terr = false;
+
+  int node_n = v.bn[nb + node];
+  double node_w = v.bw[nb + node];
+  int depth = 0;
+  for (;;) {
+    if (lane == 0) {
+      s_node[grp][depth] = node;
+      s_n[grp][depth] = node_n;
+      s_w[grp][depth] = node_w;
+    }
+    const int cb = v.bc[nb + node];
+    if (cb < 0) {  // an expanded node is required here
+      if (lane == 0) set_err(v, SPMCTS_ERR_STATE);
+      return;
+    }
+    const uint32_t vm = v.bvm[bb + cb];
+    const size_t ci = nb + (size_t)cb * P + lane;
+    int cn = 0, cc = -1;
+    double cw = 0.0;
+    float cp = 0.f;
+    if (lane < G::A) {
+      cn = v.bn[ci];
+      cw = v.bw[ci];
+      cp = v.bp[ci];
+      cc = v.bc[ci];
+    }
+    const bool valid = (lane < G::A) && ((vm >> lane) & 1u);
+    double score = -10000000000.0;  // mcts.py:347
+    if (valid) {
+      // q (mcts.py:59-62): children carry no virtual loss in sequential mode
+      const double q = cn ? cw / (double)cn : 0.0;
+      // p_eff (mcts.py:64-69): noise only on the active root's children
+      const double pe = (depth == 0 && noise) ? nz * v.x + (double)cp * (1.0 - v.x) : (double)cp;
+      // u (mcts.py:71-78): parent.n + parent.virtual_loss, and the parent holds vl = 1 here
+      const double u = ((v.cpuct * pe) * sqrt((double)(node_n + 1))) / (double)(1 + cn);
+      // select_prob (mcts.py:80-84): -child.player * q + u = parent.player * q + u
+      score = (player > 0 ? q : -q) + u;
+    }
+    if (!group_or<P>(valid ? 1 : 0)) {  // mcts.py:349-354
+      if (lane == 0) set_err(v, SPMCTS_ERR_NOCHILD);
+      return;
+    }
+    // argmax(select_probs + 1e-6 * rand(A)) (mcts.py:355): first index on ties
+    double s = -INFINITY;
+    if (lane < G::A) s = score + 0.000001 * rng_lane(v, rng, lane, &terr);
+    rng_advance(v, rng, G::A);
+    int a = lane;
+    group_argmax<P>(s, a);
+    const int gbase = (threadIdx.x & 63) & ~(P - 1);
+    const int cc_a = __shfl(cc, gbase + a, 64);
+    const int cn_a = __shfl(cn, gbase + a, 64);
+    const double cw_a = __shfl(cw, gbase + a, 64);
+    const int child = cb * P + a;
+    if (cc_a < 0) {
+      // leaf reached: _expand_node (mcts.py:301-321)
+      Board nb2 = b;
+      int rew = 0, done = 0;
+      const int st = step<G>(nb2, a, player, &rew, &done);
+      if (lane == 0) {
+        if (st != STEP_OK) set_err(v, SPMCTS_ERR_STATE);
+        int64_t *cnt = v.cnt + (size_t)tree * C_NCNT;
+        cnt[C_SIMS] += 1;
+        cnt[C_DEPTH] += depth + 1;
+        if (done) {
+          // terminal: value r (or strong_play shaping), no children, backup in place
+          const double val = terminal_value(v, b, rew * player);
+          for (int k = 0; k <= depth; ++k) {
+            const size_t idx = nb + s_node[grp][k];
+            v.bn[idx] = s_n[grp][k] + 1;
+            v.bw[idx] = s_w[grp][k] + val;
+            if (v.strong) v.bf64[idx] = 1;
+          }
+          v.bn[nb + child] = cn_a + 1;
+          v.bw[nb + child] = cw_a + val;
+          if (v.strong) v.bf64[nb + child] = 1;
+          cnt[C_TERM] += 1;
+        } else {
+          // pending network evaluation: stash the path for k_expand
+          const size_t pb = (size_t)tree * G::MAXD;
+          for (int k = 0; k <= depth; ++k) {
+            v.pnode[pb + k] = s_node[grp][k];
+            v.pn[pb + k] = s_n[grp][k];
+            v.pw[pb + k] = s_w[grp][k];
+          }
+          v.plen[tree] = depth + 1;
+          v.leaf[tree] = child;
+          v.leaf_n[tree] = cn_a;
+          v.leaf_w[tree] = cw_a;
+          v.lpos[tree] = nb2.pos;
+          v.lneg[tree] = nb2.neg;
+          v.lmover[tree] = (int8_t)player;
+          v.need[tree] = 1;
+        }
+        if (terr) set_err(v, SPMCTS_ERR_TAPE);
+        rng_store(v, tree, rng);
+      }
+      return;
+    }
+    // descend
+    play<G>(b, a, player);
+    node = child;
+    node_n = cn_a;
+    node_w = cw_a;
+    player = -player;
+    ++depth;
+    if (depth >= G::MAXD) {
+      if (lane == 0) set_err(v, SPMCTS_ERR_STATE);
+      return;
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// kernel: compaction of pending leaves into rows (tree order => deterministic)
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_scan_need(View v, int32_t *count_out) {
+  __shared__ int32_t s_part[1024];
+  const int tid = threadIdx.x;
+  const int T = v.T;
+  const int chunk = (T + 1023) / 1024;
+  const int lo = min(T, tid * chunk), hi = min(T, lo + chunk);
+  int c = 0;
+  for (int t = lo; t < hi; ++t) c += v.need[t] ? 1 : 0;
+  s_part[tid] = c;
+  __syncthreads();
+  // inclusive Hillis-Steele scan over 1024 partials
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int add = tid >= off ? s_part[tid - off] : 0;
+    __syncthreads();
+    s_part[tid] += add;
+    __syncthreads();
+  }
+  int row = s_part[tid] - c;
+  for (int t = lo; t < hi; ++t)
+    if (v.need[t]) v.row_tree[row++] = t;
+  if (tid == 1023) {
+    v.row_count[0] = s_part[1023];
+    if (count_out) count_out[0] = s_part[1023];
+  }
+}
+
+// ----------------------------------------------------------------------------
+// kernel: leaf encoding (preprocess, games/general/modules.py:115-125; input = state*mover)
+// ----------------------------------------------------------------------------
+template <class G>
+__global__ void k_encode(View v, void *out) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int row = (int)(gid / G::CELLS);
+  const int cell = (int)(gid % G::CELLS);
+  if (row >= v.row_count[0]) return;
+  const int t = v.row_tree[row];
+  const int x = cell / G::H, y = cell % G::H;
+  const uint64_t bit = 1ull << cell_bit<G>(x, y);
+  const int mover = v.lmover[t];
+  const uint64_t own = mover > 0 ? v.lpos[t] : v.lneg[t];
+  const uint64_t opp = mover > 0 ? v.lneg[t] : v.lpos[t];
+  const int c_own = (own & bit) ? 1 : 0, c_opp = (opp & bit) ? 1 : 0;
+  const int c_emp = 1 - c_own - c_opp;
+  if (v.leaf_format == SPMCTS_LEAF_BOARD_I64) {
+    ((int64_t *)out)[(size_t)row * G::CELLS + cell] = (int64_t)(c_own - c_opp);
+    return;
+  }
+  size_t i0, i1, i2;
+  if (v.leaf_layout == SPMCTS_NHWC) {
+    const size_t base = ((size_t)row * G::CELLS + cell) * 3;
+    i0 = base;
+    i1 = base + 1;
+    i2 = base + 2;
+  } else {
+    const size_t base = (size_t)row * 3 * G::CELLS + cell;
+    i0 = base;
+    i1 = base + G::CELLS;
+    i2 = base + 2 * G::CELLS;
+  }
+  if (v.leaf_format == SPMCTS_LEAF_F32) {
+    float *o = (float *)out;
+    o[i0] = (float)c_emp;
+    o[i1] = (float)c_own;
+    o[i2] = (float)c_opp;
+  } else {
+    const uint16_t one = v.leaf_format == SPMCTS_LEAF_F16 ? 0x3C00 : 0x3F80;
+    uint16_t *o = (uint16_t *)out;
+    o[i0] = c_emp ? one : 0;
+    o[i1] = c_own ? one : 0;
+    o[i2] = c_opp ? one : 0;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// kernel: expand + backup of network-evaluated leaves (mcts.py:316-321, :94-98)
+// ----------------------------------------------------------------------------
+template <class G>
+__global__ __launch_bounds__(64) void k_expand(View v, const float *probs, const float *values) {
+  constexpr int P = G::APAD;
+  const int lane = threadIdx.x & (P - 1);
+  const int row = (blockIdx.x * blockDim.x + threadIdx.x) / P;
+  if (row >= v.row_count[0]) return;
+  const int tree = v.row_tree[row];
+  const size_t nb = nbase<G>(v, tree);
+  const size_t bb = (size_t)tree * v.cap;
+  const int blk = v.used[tree];
+  if (blk >= v.cap) {
+    if (lane == 0) set_err(v, SPMCTS_ERR_POOL);
+    return;
+  }
+  const int leaf = v.leaf[tree];
+  // create_children (mcts.py:103-107): A children in action order, validity = valid_moves
+  {
+    const size_t ci = nb + (size_t)blk * P + lane;
+    v.bn[ci] = 0;
+    v.bw[ci] = 0.0;
+    v.bp[ci] = lane < G::A ? probs[(size_t)row * G::A + lane] : 0.f;
+    v.bc[ci] = -1;
+    v.bf64[ci] = 0;
+  }
+  const int mover = v.lmover[tree];
+  // network(s, parent.player) returns value * player (modules.py:109-112)
+  const double val = (double)values[row] * (double)mover;
+  const int plen = v.plen[tree];
+  const size_t pb = (size_t)tree * G::MAXD;
+  for (int k = lane; k < plen; k += P) {
+    const size_t idx = nb + v.pnode[pb + k];
+    v.bn[idx] = v.pn[pb + k] + 1;
+    v.bw[idx] = v.pw[pb + k] + val;
+  }
+  if (lane == 0) {
+    v.bvm[bb + blk] = legal_mask<G>(Board{v.lpos[tree], v.lneg[tree]});
+    v.bc[nb + leaf] = blk;
+    v.bn[nb + leaf] = v.leaf_n[tree] + 1;
+    v.bw[nb + leaf] = v.leaf_w[tree] + val;
+    v.used[tree] = blk + 1;
+    v.need[tree] = 0;
+    v.cnt[(size_t)tree * C_NCNT + C_NN] += 1;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// _play (mcts.py:272-299): choose the move from root visit counts
+// ----------------------------------------------------------------------------
+struct PlayOut {
+  int action;
+  bool recorded;
+  double q;
+  uint8_t qf64;
+};
+
+// numpy kahan_sum used by RandomState.choice's validation
+__device__ __forceinline__ double kahan_sum(const double *p, int n) {
+  double s = p[0], c = 0.0;
+  for (int i = 1; i < n; ++i) {
+    const double y = p[i] - c;
+    const double t = s + y;
+    c = (t - s) - y;
+    s = t;
+  }
+  return s;
+}
+
+template <class G>
+__device__ PlayOut play_move_choice(const View &v, int tree, double temp, float *probs_out) {
+  constexpr int P = G::APAD;
+  const size_t nb = nbase<G>(v, tree);
+  const int root = v.root[tree];
+  const int cb = v.bc[nb + root];
+  PlayOut o{0, false, 0.0, 0};
+  int n[G::A];
+  for (int j = 0; j < G::A; ++j) n[j] = cb >= 0 ? v.bn[nb + (size_t)cb * P + j] : 0;
+  double t = temp;
+  if (v.evaluate) t = t / 20.0;
+  const double inv = 1.0 / t;
+  double pp[G::A];
+  for (int j = 0; j < G::A; ++j) pp[j] = inv == 1.0 ? (double)n[j] : pow((double)n[j], inv);
+  double s = 0.0;
+  for (int j = 0; j < G::A; ++j) s = s + pp[j];
+  double pr[G::A];
+  for (int j = 0; j < G::A; ++j) pr[j] = pp[j] / s;
+  // np.random.choice(A, p) validation (ValueError -> argmax fallback, mcts.py:290-295)
+  bool ok = true;
+  for (int j = 0; j < G::A; ++j)
+    if (pr[j] < 0.0 || pr[j] != pr[j]) ok = false;
+  if (ok && fabs(kahan_sum(pr, G::A) - 1.0) > 1.4901161193847656e-08) ok = false;
+  if (ok) {
+    TreeRng r;
+    rng_load(v, tree, r);
+    bool terr = false;
+    const double u = rng_next(v, r, &terr);
+    rng_store(v, tree, r);
+    if (terr) set_err(v, SPMCTS_ERR_TAPE);
+    double cdf[G::A];
+    double c = 0.0;
+    for (int j = 0; j < G::A; ++j) {
+      c = c + pr[j];
+      cdf[j] = c;
+    }
+    const double last = cdf[G::A - 1];
+    int a = 0;
+    for (int j = 0; j < G::A; ++j) {
+      cdf[j] = cdf[j] / last;
+      if (cdf[j] <= u) a = j + 1;  // searchsorted(u, side='right') on a non-decreasing cdf
+    }
+    if (a >= G::A) a = G::A - 1;
+    o.action = a;
+    o.recorded = true;
+    for (int j = 0; j < G::A; ++j) probs_out[j] = (float)pr[j];
+    const int rn = v.bn[nb + root];
+    o.q = rn ? v.bw[nb + root] / (double)rn : 0.0;
+    o.qf64 = v.bf64[nb + root];
+  } else {
+    int best = 0;
+    for (int j = 1; j < G::A; ++j)
+      if (n[j] > n[best]) best = j;
+    o.action = best;
+  }
+  v.noise_on[tree] = 0;  // remove_noise (mcts.py:55-57)
+  v.cnt[(size_t)tree * C_NCNT + C_MOVES] += 1;
+  return o;
+}
+
+template <class G>
+__device__ __forceinline__ void write_state(Board b, int8_t *dst) {
+  for (int x = 0; x < G::W; ++x)
+    for (int y = 0; y < G::H; ++y) dst[x * G::H + y] = cell_value<G>(b, x, y);
+}
+
+template <class G>
+__global__ void k_search_end(View v, int n_active, double temp, int32_t *actions, int8_t *states, float *tprobs,
+                             double *qs, uint8_t *qf64, uint8_t *recorded) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_active) return;
+  const int tree = v.active[i];
+  if (tree < 0) return;
+  float pr[G::A];
+  const PlayOut o = play_move_choice<G>(v, tree, temp, pr);
+  actions[i] = o.action;
+  recorded[i] = o.recorded ? 1 : 0;
+  qs[i] = o.q;
+  qf64[i] = o.qf64;
+  for (int j = 0; j < G::A; ++j) tprobs[(size_t)i * G::A + j] = o.recorded ? pr[j] : 0.f;
+  write_state<G>(Board{v.rpos[tree], v.rneg[tree]}, states + (size_t)i * G::CELLS);
+}
+
+// _set_node (mcts.py:201-209) for one tree; returns false on an illegal action.
+template <class G>
+__device__ bool set_node(const View &v, int tree, int a) {
+  constexpr int P = G::APAD;
+  const size_t nb = nbase<G>(v, tree);
+  const size_t bb = (size_t)tree * v.cap;
+  const int root = v.root[tree];
+  const int cb = v.bc[nb + root];
+  if (cb < 0 || a < 0 || a >= G::A || !((v.bvm[bb + cb] >> a) & 1u)) {
+    set_err(v, SPMCTS_ERR_ACTION);
+    return false;
+  }
+  const int child = cb * P + a;
+  const int rp = v.rplayer[tree];
+  Board b{v.rpos[tree], v.rneg[tree]};
+  int rew = 0, done = 0;
+  step<G>(b, a, rp, &rew, &done);
+  if (v.bn[nb + child] == 0) {
+    int64_t *cnt = v.cnt + (size_t)tree * C_NCNT;
+    cnt[C_SETNODE] += 1;
+    if (done) {
+      const double val = terminal_value(v, Board{v.rpos[tree], v.rneg[tree]}, rew * rp);
+      v.bn[nb + child] = 1;
+      v.bw[nb + child] = v.bw[nb + child] + val;
+      if (v.strong) v.bf64[nb + child] = 1;
+    } else {
+      v.plen[tree] = 0;
+      v.leaf[tree] = child;
+      v.leaf_n[tree] = 0;
+      v.leaf_w[tree] = v.bw[nb + child];
+      v.lpos[tree] = b.pos;
+      v.lneg[tree] = b.neg;
+      v.lmover[tree] = (int8_t)rp;
+      v.need[tree] = 1;
+    }
+  }
+  v.root[tree] = child;
+  v.rpos[tree] = b.pos;
+  v.rneg[tree] = b.neg;
+  v.rplayer[tree] = (int8_t)(-rp);
+  return true;
+}
+
+template <class G>
+__global__ void k_play_action(View v, const int32_t *trees, const int32_t *actions, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int t = trees[i];
+  if (t < 0 || t >= v.T) return;
+  set_node<G>(v, t, actions[i]);
+}
+
+// ----------------------------------------------------------------------------
+// games: SelfPlayer.play_episode state machine (selfplayworker.py:164-224)
+// ----------------------------------------------------------------------------
+template <class G>
+__device__ void start_game(const View &v, int g, int64_t id, const float *priors) {
+  const bool swap = (id & 1) != 0;  // swap_sides = not i % 2 == 0 (self_play_parallel.py:237)
+  v.gpos[g] = 0;
+  v.gneg[g] = 0;
+  v.gply[g] = 0;
+  v.gswap[g] = swap ? 1 : 0;
+  v.gstate[g] = GS_ACTIVE;
+  v.gresult[g] = 0;
+  v.gid[g] = id;
+  v.mv_count[2 * g] = 0;
+  v.mv_count[2 * g + 1] = 0;
+  // policy.reset(-1 if swap else 1), opposing.reset(1 if swap else -1)  (:175-176)
+  reset_tree<G>(v, 2 * g, swap ? -1 : 1, priors ? priors : v.root_prior);
+  reset_tree<G>(v, 2 * g + 1, swap ? 1 : -1, priors ? priors + G::A : v.root_prior);
+}
+
+template <class G>
+__global__ void k_games_start(View v, const int32_t *slots, const float *priors, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int g = slots[i];
+  if (g < 0 || g >= v.G) {
+    set_err(v, SPMCTS_ERR_STATE);
+    return;
+  }
+  start_game<G>(v, g, v.gcnt[7] + i, priors ? priors + (size_t)i * 2 * G::A : nullptr);
+}
+
+__global__ void k_games_bump_id(View v, int n) { v.gcnt[7] += n; }
+
+template <class G>
+__global__ void k_games_begin_ply(View v) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= v.G) return;
+  if (v.gstate[g] != GS_ACTIVE) {
+    v.active[g] = -1;
+    return;
+  }
+  // policy moves on even plies unless swap_sides (:178-183)
+  const int mover = (v.gply[g] + v.gswap[g]) & 1;
+  const int tree = 2 * g + mover;
+  v.active[g] = tree;
+  draw_noise<G>(v, tree);
+}
+
+template <class G>
+__global__ void k_games_end_ply(View v) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= v.G) return;
+  if (v.gstate[g] != GS_ACTIVE) return;
+  const int mover = (v.gply[g] + v.gswap[g]) & 1;
+  const int tree = 2 * g + mover;
+  const int m = v.mv_count[tree];
+  float pr[G::A];
+  const PlayOut o = play_move_choice<G>(v, tree, 1.0, pr);
+  if (o.recorded) {
+    if (m < G::MAXM) {
+      const size_t rec = (size_t)tree * G::MAXM + m;
+      write_state<G>(Board{v.rpos[tree], v.rneg[tree]}, v.mv_state + rec * G::CELLS);
+      for (int j = 0; j < G::A; ++j) v.mv_probs[rec * G::A + j] = pr[j];
+      v.mv_q[rec] = o.q;
+      v.mv_qf64[rec] = o.qf64;
+      v.mv_count[tree] = m + 1;
+    } else {
+      set_err(v, SPMCTS_ERR_STATE);
+    }
+  }
+  // env.step in the policy's frame (play_move :221-224): policy plays +1, opponent -1
+  const int p_env = mover == 0 ? 1 : -1;
+  Board gb{v.gpos[g], v.gneg[g]};
+  int rew = 0, done = 0;
+  const int st = step<G>(gb, o.action, p_env, &rew, &done);
+  if (st != STEP_OK) set_err(v, SPMCTS_ERR_ACTION);
+  v.gpos[g] = gb.pos;
+  v.gneg[g] = gb.neg;
+  v.gply[g] += 1;
+  if (done) {
+    v.gstate[g] = GS_DONE;
+    v.gresult[g] = (int8_t)(rew * p_env);  // r = r * player (:218)
+    return;  // both trees are discarded with the game
+  }
+  set_node<G>(v, 2 * g, o.action);
+  set_node<G>(v, 2 * g + 1, o.action);
+}
+
+// finished games: offsets into the export ring + refill ids (single block, slot order)
+template <class G>
+__global__ __launch_bounds__(1024) void k_games_finish_scan(View v, int refill, int32_t *out) {
+  __shared__ int32_t s_rec[1024];
+  __shared__ int32_t s_fin[1024];
+  const int tid = threadIdx.x;
+  const int Gn = v.G;
+  const int chunk = (Gn + 1023) / 1024;
+  const int lo = min(Gn, tid * chunk), hi = min(Gn, lo + chunk);
+  int rec = 0, fin = 0;
+  for (int g = lo; g < hi; ++g)
+    if (v.gstate[g] == GS_DONE) {
+      rec += v.mv_count[2 * g] + v.mv_count[2 * g + 1];
+      fin += 1;
+    }
+  s_rec[tid] = rec;
+  s_fin[tid] = fin;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int a1 = tid >= off ? s_rec[tid - off] : 0;
+    const int a2 = tid >= off ? s_fin[tid - off] : 0;
+    __syncthreads();
+    s_rec[tid] += a1;
+    s_fin[tid] += a2;
+    __syncthreads();
+  }
+  const int base_rec = v.ex_count[0];
+  int r0 = base_rec + s_rec[tid] - rec;
+  int f0 = s_fin[tid] - fin;
+  // per-game: record offset and finish index (for refill ids) in gscratch[2*g], [2*g+1]
+  for (int g = lo; g < hi; ++g)
+    if (v.gstate[g] == GS_DONE) {
+      v.gscratch[2 * g] = r0;
+      v.gscratch[2 * g + 1] = f0;
+      r0 += v.mv_count[2 * g] + v.mv_count[2 * g + 1];
+      f0 += 1;
+    }
+  __syncthreads();
+  if (tid == 0) {
+    const int total_rec = s_rec[1023], total_fin = s_fin[1023];
+    int64_t started = v.gcnt[7];
+    int64_t limit = v.gcnt[8];
+    int64_t can = 0;
+    if (refill) {
+      if (limit < 0) {
+        can = total_fin;
+      } else {
+        const int64_t room = limit - started;
+        can = room < 0 ? 0 : (room < (int64_t)total_fin ? room : (int64_t)total_fin);
+      }
+    }
+    v.gscratch[2 * Gn] = (int32_t)can;     // refills this ply
+    v.gscratch[2 * Gn + 1] = (int32_t)(started & 0x7fffffff);
+    ((int64_t *)(v.gscratch + 2 * Gn + 2))[0] = started;
+    v.gcnt[7] = started + can;
+    v.gcnt[0] += total_fin;
+    if (base_rec + total_rec > v.ex_cap) atomicOr(v.err, SPMCTS_ERR_EXPORT);
+    v.ex_count[0] = min(v.ex_cap, base_rec + total_rec);
+    v.gcnt[9] += min(total_rec, v.ex_cap - base_rec);
+    if (out) {
+      out[0] = total_fin;
+      out[1] = v.ex_count[0];
+    }
+  }
+}
+
+template <class G>
+__global__ void k_games_finish_apply(View v) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= v.G) return;
+  if (v.gstate[g] != GS_DONE) return;
+  const int r = v.gresult[g];
+  const int swap = v.gswap[g];
+  // results breakdown (self_play_parallel.py:302-327): reward in the policy's view
+  atomicAdd((unsigned long long *)&v.gcnt[1 + swap * 3 + (r == 1 ? 0 : (r == 0 ? 1 : 2))], 1ull);
+  // push_to_queue: policy's moves with r, then opposing's with -r (selfplayworker.py:186-190)
+  int off = v.gscratch[2 * g];
+  for (int side = 0; side < 2; ++side) {
+    const int tree = 2 * g + side;
+    const float z = side == 0 ? (float)r : (float)(-r);
+    const int m = v.mv_count[tree];
+    for (int k = 0; k < m; ++k, ++off) {
+      if (off >= v.ex_cap) continue;
+      const size_t src = (size_t)tree * G::MAXM + k;
+      for (int c = 0; c < G::CELLS; ++c) v.ex_state[(size_t)off * G::CELLS + c] = v.mv_state[src * G::CELLS + c];
+      for (int j = 0; j < G::A; ++j) v.ex_probs[(size_t)off * G::A + j] = v.mv_probs[src * G::A + j];
+      v.ex_q[off] = v.mv_q[src];
+      v.ex_qf64[off] = v.mv_qf64[src];
+      v.ex_z[off] = z;
+      v.ex_game[off] = v.gid[g];
+    }
+  }
+  const int fin_idx = v.gscratch[2 * g + 1];
+  const int can = v.gscratch[2 * v.G];
+  const int64_t started = ((const int64_t *)(v.gscratch + 2 * v.G + 2))[0];
+  if (fin_idx < can) {
+    start_game<G>(v, g, started + fin_idx, nullptr);
+  } else {
+    v.gstate[g] = GS_IDLE;
+  }
+}
+
+__global__ void k_export(View v, int A, int cells, int8_t *st, float *pr, double *q, uint8_t *qf, float *z, int64_t *gid,
+                         int max_records, int32_t *count_out) {
+  const int n = min(v.ex_count[0], max_records);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0 && count_out) count_out[0] = n;
+  if (i >= n) return;
+  for (int c = 0; c < cells; ++c) st[(size_t)i * cells + c] = v.ex_state[(size_t)i * cells + c];
+  for (int j = 0; j < A; ++j) pr[(size_t)i * A + j] = v.ex_probs[(size_t)i * A + j];
+  q[i] = v.ex_q[i];
+  qf[i] = v.ex_qf64[i];
+  z[i] = v.ex_z[i];
+  gid[i] = v.ex_game[i];
+}
+
+__global__ void k_export_clear(View v) { v.ex_count[0] = 0; }
+
+// ----------------------------------------------------------------------------
+// stand-alone kernels
+// ----------------------------------------------------------------------------
+template <class G>
+__global__ void k_env_step(const int8_t *boards, const int32_t *actions, const int8_t *players, const uint8_t *over,
+                           int n, int8_t *out, int8_t *reward, uint8_t *done, int8_t *status, uint8_t *valid) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Board b = from_cells<G>(boards + (size_t)i * G::CELLS);
+  int rew = 0, dn = 0, st;
+  if (over && over[i]) {
+    st = STEP_GAME_OVER;
+    dn = 1;
+  } else {
+    st = step<G>(b, actions[i], players[i], &rew, &dn);
+  }
+  for (int x = 0; x < G::W; ++x)
+    for (int y = 0; y < G::H; ++y) out[(size_t)i * G::CELLS + x * G::H + y] = cell_value<G>(b, x, y);
+  reward[i] = (int8_t)rew;
+  done[i] = (uint8_t)dn;
+  status[i] = (int8_t)st;
+  const uint32_t lm = legal_mask<G>(b);
+  for (int a = 0; a < G::A; ++a) valid[(size_t)i * G::A + a] = (lm >> a) & 1u;
+}
+
+// table network (oracle/table_net.py) from leaf rows
+template <class G>
+__global__ void k_table_net(const void *leaves, int fmt, int layout, int n, uint64_t salt, const uint64_t *salts,
+                            float *probs, float *values) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t h = 0xCBF29CE484222325ull;
+  for (int cell = 0; cell < G::CELLS; ++cell) {
+    int c = 0;
+    if (fmt == SPMCTS_LEAF_BOARD_I64) {
+      const int64_t val = ((const int64_t *)leaves)[(size_t)i * G::CELLS + cell];
+      c = val == 1 ? 1 : (val == -1 ? 2 : 0);
+    } else {
+      size_t i1, i2;
+      if (layout == SPMCTS_NHWC) {
+        i1 = ((size_t)i * G::CELLS + cell) * 3 + 1;
+        i2 = i1 + 1;
+      } else {
+        i1 = (size_t)i * 3 * G::CELLS + G::CELLS + cell;
+        i2 = i1 + G::CELLS;
+      }
+      float own, opp;
+      if (fmt == SPMCTS_LEAF_F32) {
+        own = ((const float *)leaves)[i1];
+        opp = ((const float *)leaves)[i2];
+      } else {
+        own = ((const uint16_t *)leaves)[i1] ? 1.f : 0.f;
+        opp = ((const uint16_t *)leaves)[i2] ? 1.f : 0.f;
+      }
+      c = own != 0.f ? 1 : (opp != 0.f ? 2 : 0);
+    }
+    h = (h ^ (uint64_t)(c + 3 * cell + 1)) * 0x100000001B3ull;
+  }
+  h ^= salts ? salts[i] : salt;
+  uint32_t k[G::A];
+  uint32_t tot = 0;
+  for (int j = 0; j < G::A; ++j) {
+    k[j] = 1u + (uint32_t)((splitmix64(h + (uint64_t)j) >> 40) & 0xFFFFull);
+    tot += k[j];
+  }
+  const float ft = (float)tot;
+  for (int j = 0; j < G::A; ++j) probs[(size_t)i * G::A + j] = __fdiv_rn((float)k[j], ft);
+  const int raw = (int)((splitmix64(h ^ 0x5DEECE66Dull) >> 40) & 0xFFFFull) - 32768;
+  values[i] = __fdiv_rn((float)raw, 32768.0f);
+}
+
+__global__ void k_copy_probe(const float4 *src, float4 *dst, size_t n4) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (; i < n4; i += stride) dst[i] = src[i];
+}
+
+// ----------------------------------------------------------------------------
+// host side
+// ----------------------------------------------------------------------------
+struct spmcts_arena {
+  spmcts_config cfg;
+  int device;
+  int A, W, H, P, cells, maxd, maxm;
+  View v;
+  std::vector<void *> allocs;
+  int n_active;  // active-set size for select / search_end
+};
+
+static int geometry(const spmcts_config *c, int *A, int *P, int *cells, int *maxd, int *maxm) {
+  if (c->game == SPMCTS_CONNECT4 && c->width == 7 && c->height == 6) {
+    *A = C4::A; *P = C4::APAD; *cells = C4::CELLS; *maxd = C4::MAXD; *maxm = C4::MAXM;
+    return 0;
+  }
+  if (c->game == SPMCTS_TICTACTOE && c->width == 3 && c->height == 3) {
+    *A = TTT::A; *P = TTT::APAD; *cells = TTT::CELLS; *maxd = TTT::MAXD; *maxm = TTT::MAXM;
+    return 0;
+  }
+  return fail(-2, "unsupported game/board size (instantiated: connect4 7x6, tictactoe 3x3)");
+}
+
+// worst-case node blocks per tree per game: root pseudo block + root children + one
+// block per expansion; a tree searches at most ceil(cells/2) times and play_action
+// expands at most once per ply.
+static int default_cap(const spmcts_config *c, int cells) {
+  const long long it = std::max(1, c->iterations);
+  const long long cap = 2 + ((cells + 1) / 2) * it + cells + 2;
+  return (int)std::min<long long>(cap, 1 << 26);
+}
+
+struct Plan {
+  size_t off = 0;
+  std::vector<std::pair<void **, size_t>> items;
+  template <class T>
+  void add(T **p, size_t count) {
+    items.push_back({(void **)p, sizeof(T) * std::max<size_t>(count, 1)});
+  }
+  size_t total() const {
+    size_t t = 0;
+    for (auto &it : items) t += (it.second + 255) & ~size_t(255);
+    return t;
+  }
+};
+
+static void plan_arena(spmcts_arena *h, Plan &pl) {
+  View &v = h->v;
+  const size_t T = v.T, P = h->P, cap = v.cap, G = v.G;
+  const size_t nodes = T * cap * P;
+  pl.add(&v.bn, nodes);
+  pl.add(&v.bw, nodes);
+  pl.add(&v.bp, nodes);
+  pl.add(&v.bc, nodes);
+  pl.add(&v.bf64, nodes);
+  pl.add(&v.bvm, T * cap);
+  pl.add(&v.root, T);
+  pl.add(&v.rpos, T);
+  pl.add(&v.rneg, T);
+  pl.add(&v.rplayer, T);
+  pl.add(&v.used, T);
+  pl.add(&v.noise, T * P);
+  pl.add(&v.noise_on, T);
+  pl.add(&v.pnode, T * h->maxd);
+  pl.add(&v.pn, T * h->maxd);
+  pl.add(&v.pw, T * h->maxd);
+  pl.add(&v.plen, T);
+  pl.add(&v.leaf, T);
+  pl.add(&v.leaf_n, T);
+  pl.add(&v.leaf_w, T);
+  pl.add(&v.lpos, T);
+  pl.add(&v.lneg, T);
+  pl.add(&v.lmover, T);
+  pl.add(&v.need, T);
+  pl.add(&v.rng, T);
+  pl.add((int64_t **)&v.tape_end, T);
+  pl.add(&v.tape_cur, T);
+  pl.add(&v.cnt, T * C_NCNT);
+  pl.add(&v.active, std::max(T, G));
+  pl.add(&v.row_tree, T);
+  pl.add(&v.row_count, 4);
+  pl.add(&v.root_prior, 16);
+  pl.add(&v.err, 4);
+  pl.add(&v.gpos, G);
+  pl.add(&v.gneg, G);
+  pl.add(&v.gply, G);
+  pl.add(&v.gswap, G);
+  pl.add(&v.gstate, G);
+  pl.add(&v.gresult, G);
+  pl.add(&v.gid, G);
+  pl.add(&v.mv_state, 2 * G * h->maxm * h->cells);
+  pl.add(&v.mv_probs, 2 * G * h->maxm * h->A);
+  pl.add(&v.mv_q, 2 * G * h->maxm);
+  pl.add(&v.mv_qf64, 2 * G * h->maxm);
+  pl.add(&v.mv_count, 2 * G);
+  const size_t X = std::max<size_t>(64, 4 * G * h->maxm);
+  v.ex_cap = (int32_t)X;
+  pl.add(&v.ex_state, X * h->cells);
+  pl.add(&v.ex_probs, X * h->A);
+  pl.add(&v.ex_q, X);
+  pl.add(&v.ex_qf64, X);
+  pl.add(&v.ex_z, X);
+  pl.add(&v.ex_game, X);
+  pl.add(&v.ex_count, 4);
+  pl.add(&v.gcnt, 16);
+  pl.add(&v.gscratch, 2 * G + 8);
+}
+
+static int setup_view(spmcts_arena *h, const spmcts_config *cfg) {
+  int A, P, cells, maxd, maxm;
+  if (geometry(cfg, &A, &P, &cells, &maxd, &maxm)) return -2;
+  h->cfg = *cfg;
+  h->A = A;
+  h->P = P;
+  h->cells = cells;
+  h->maxd = maxd;
+  h->maxm = maxm;
+  h->W = cfg->width;
+  h->H = cfg->height;
+  View &v = h->v;
+  memset(&v, 0, sizeof(v));
+  v.T = cfg->n_trees;
+  v.G = cfg->n_games;
+  v.A = A;
+  v.cap = cfg->blocks_per_tree > 0 ? cfg->blocks_per_tree : default_cap(cfg, cells);
+  v.cpuct = cfg->cpuct;
+  v.x = cfg->x_noise;
+  v.alpha = cfg->alpha;
+  v.strong = cfg->strong_play;
+  v.evaluate = cfg->evaluate;
+  v.rng_mode = cfg->rng_mode;
+  v.leaf_format = cfg->leaf_format;
+  v.leaf_layout = cfg->leaf_layout;
+  if (v.T <= 0) return fail(-3, "n_trees must be > 0");
+  if (v.G < 0 || 2 * (long long)v.G > v.T) return fail(-3, "games mode needs n_trees >= 2 * n_games");
+  if (v.T > (1 << 24)) return fail(-3, "too many trees");
+  if (v.cap < 4) return fail(-3, "blocks_per_tree too small");
+  if ((long long)v.cap * P >= (1ll << 31)) return fail(-3, "blocks_per_tree too large");
+  return 0;
+}
+
+__global__ void k_rng_init(View v, uint64_t seed, uint64_t sub0) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= v.T) return;
+  Philox s;
+  rocrand_init(seed, sub0 + (uint64_t)t, 0ull, &s);
+  v.rng[t] = s;
+  v.tape_cur[t] = 0;
+  ((int64_t *)v.tape_end)[t] = 0;
+  v.need[t] = 0;
+  v.noise_on[t] = 0;
+  for (int k = 0; k < C_NCNT; ++k) v.cnt[(size_t)t * C_NCNT + k] = 0;
+}
+
+__global__ void k_games_init(View v) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g == 0) {
+    for (int k = 0; k < 16; ++k) v.gcnt[k] = 0;
+    v.gcnt[8] = -1;  // unlimited refill
+    v.ex_count[0] = 0;
+    v.err[0] = 0;
+    v.row_count[0] = 0;
+  }
+  if (g >= v.G) return;
+  v.gstate[g] = GS_IDLE;
+  v.mv_count[2 * g] = 0;
+  v.mv_count[2 * g + 1] = 0;
+}
+
+#define DISPATCH(h, KCALL)                                             \
+  do {                                                                 \
+    if ((h)->cfg.game == SPMCTS_CONNECT4) {                            \
+      using GG = C4;                                                   \
+      KCALL;                                                           \
+    } else {                                                           \
+      using GG = TTT;                                                  \
+      KCALL;                                                           \
+    }                                                                  \
+  } while (0)
+
+static inline int nblk(long long n, int b) { return (int)std::max<long long>(1, (n + b - 1) / b); }
+
+__global__ void k_set_tape(View v, const int64_t *offsets) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= v.T) return;
+  v.tape_cur[t] = offsets[t];
+  ((int64_t *)v.tape_end)[t] = offsets[t + 1];
+}
+
+template <class G>
+static int env_step_host_t(int8_t *board, int32_t action, int32_t player, int32_t *reward, int32_t *done) {
+  Board b = from_cells<G>(board);
+  int r = 0, d = 0;
+  const int st = step<G>(b, action, player, &r, &d);
+  for (int x = 0; x < G::W; ++x)
+    for (int y = 0; y < G::H; ++y) board[x * G::H + y] = cell_value<G>(b, x, y);
+  *reward = r;
+  *done = d;
+  return st;
+}
+
+extern "C" {
+
+int spmcts_version(void) { return 1; }
+
+const char *spmcts_last_error(void) { return g_last_error.c_str(); }
+
+int spmcts_arena_bytes(const spmcts_config *cfg, uint64_t *bytes_out) {
+  spmcts_arena tmp;
+  if (setup_view(&tmp, cfg)) return -2;
+  Plan pl;
+  plan_arena(&tmp, pl);
+  *bytes_out = pl.total();
+  return 0;
+}
+
+int spmcts_arena_create(const spmcts_config *cfg, int device, spmcts_arena **out) {
+  if (!cfg || !out) return fail(-1, "null argument");
+  spmcts_arena *h = new spmcts_arena();
+  h->device = device;
+  h->n_active = 0;
+  int rc = setup_view(h, cfg);
+  if (rc) {
+    delete h;
+    return rc;
+  }
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) {
+    delete h;
+    return fail(-1000 - (int)e, std::string("hipSetDevice: ") + hipGetErrorString(e));
+  }
+  Plan pl;
+  plan_arena(h, pl);
+  for (auto &it : pl.items) {
+    void *p = nullptr;
+    e = hipMalloc(&p, it.second);
+    if (e != hipSuccess) {
+      for (void *q : h->allocs) (void)hipFree(q);
+      delete h;
+      return fail(-1000 - (int)e, std::string("hipMalloc: ") + hipGetErrorString(e));
+    }
+    h->allocs.push_back(p);
+    *it.first = p;
+  }
+  hipLaunchKernelGGL(k_rng_init, dim3(nblk(h->v.T, 256)), dim3(256), 0, 0, h->v, cfg->seed, cfg->subsequence0);
+  hipLaunchKernelGGL(k_games_init, dim3(nblk(std::max(1, h->v.G), 256)), dim3(256), 0, 0, h->v);
+  // default root prior: uniform (replaced by spmcts_set_root_prior)
+  std::vector<float> pri(16, 0.f);
+  for (int j = 0; j < h->A; ++j) pri[j] = 1.0f / h->A;
+  e = hipMemcpy(h->v.root_prior, pri.data(), 16 * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    for (void *q : h->allocs) (void)hipFree(q);
+    delete h;
+    return fail(-1000 - (int)e, std::string("arena init: ") + hipGetErrorString(e));
+  }
+  *out = h;
+  return 0;
+}
+
+int spmcts_arena_destroy(spmcts_arena *h) {
+  if (!h) return 0;
+  (void)hipSetDevice(h->device);
+  (void)hipDeviceSynchronize();
+  for (void *p : h->allocs) (void)hipFree(p);
+  delete h;
+  return 0;
+}
+
+int spmcts_arena_geometry(const spmcts_arena *h, int32_t *A, int32_t *W, int32_t *H, int32_t *bpt, int32_t *nt,
+                          int32_t *ng) {
+  if (!h) return fail(-1, "null arena");
+  if (A) *A = h->A;
+  if (W) *W = h->W;
+  if (H) *H = h->H;
+  if (bpt) *bpt = h->v.cap;
+  if (nt) *nt = h->v.T;
+  if (ng) *ng = h->v.G;
+  return 0;
+}
+
+int spmcts_set_root_prior(spmcts_arena *h, const float *probs_dev, spmcts_stream stream) {
+  if (!h || !probs_dev) return fail(-1, "null argument");
+  HIP_TRY(hipMemcpyAsync(h->v.root_prior, probs_dev, sizeof(float) * h->A, hipMemcpyDeviceToDevice,
+                         (hipStream_t)stream));
+  return 0;
+}
+
+int spmcts_set_tape(spmcts_arena *h, const double *tape_dev, const int64_t *offsets_dev, spmcts_stream stream) {
+  if (!h || !offsets_dev) return fail(-1, "null argument");
+  if (h->cfg.rng_mode != SPMCTS_RNG_TAPE) return fail(-4, "arena is not in tape RNG mode");
+  h->v.tape = tape_dev;
+  hipLaunchKernelGGL(k_set_tape, dim3(nblk(h->v.T, 256)), dim3(256), 0, (hipStream_t)stream, h->v, offsets_dev);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int spmcts_tree_reset(spmcts_arena *h, const int32_t *trees_dev, const int8_t *root_player_dev,
+                      const float *priors_dev, int32_t n, spmcts_stream stream) {
+  if (!h) return fail(-1, "null arena");
+  if (n <= 0) return 0;
+  DISPATCH(h, hipLaunchKernelGGL(k_tree_reset<GG>, dim3(nblk(n, 128)), dim3(128), 0, (hipStream_t)stream, h->v,
+                                 trees_dev, root_player_dev, priors_dev, n));
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int spmcts_search_begin(spmcts_arena *h, const int32_t *trees_dev, int32_t n, spmcts_stream stream) {
+  if (!h) return fail(-1, "null arena");
+  if (n > std::max(h->v.T, h->v.G)) return fail(-3, "too many active trees");
+  h->n_active = n;
+  if (n <= 0) return 0;
+  DISPATCH(h, hipLaunchKernelGGL(k_search_begin<GG>, dim3(nblk(n, 128)), dim3(128), 0, (hipStream_t)stream, h->v,
+                                 trees_dev, n));
+  LAUNCH_CHECK();
+  return 0;
+}
+
+static int launch_rows(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_dev, hipStream_t s) {
+  hipLaunchKernelGGL(k_scan_need, dim3(1), dim3(1024), 0, s, h->v, leaf_count_dev);
+  if (leaves_dev) {
+    const long long total = (long long)h->v.T * h->cells;
+    DISPATCH(h, hipLaunchKernelGGL(k_encode<GG>, dim3(nblk(total, 256)), dim3(256), 0, s, h->v, leaves_dev));
+  }
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int spmcts_select_tree(spmcts_arena *h, spmcts_stream stream) {
+  if (!h) return fail(-1, "null arena");
+  hipStream_t s = (hipStream_t)stream;
+  const int n = h->n_active;
+  if (n > 0) {
+    const int gpb = 64 / h->P;
+    DISPATCH(h, hipLaunchKernelGGL(k_select<GG>, dim3(nblk(n, gpb)), dim3(64), 0, s, h->v, n));
+  }
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int spmcts_leaf_rows(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_dev, spmcts_stream stream) {
+  if (!h) return fail(-1, "null arena");
+  return launch_rows(h, leaves_dev, leaf_count_dev, (hipStream_t)stream);
+}
+
+int spmcts_select(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_dev, spmcts_stream stream) {
+  const int rc = spmcts_select_tree(h, stream);
+  if (rc) return rc;
+  return spmcts_leaf_rows(h, leaves_dev, leaf_count_dev, stream);
+}
+
+int spmcts_expand(spmcts_arena *h, const float *probs_dev, const float *values_dev, spmcts_stream stream) {
+  if (!h) return fail(-1, "null arena");
+  const int gpb = 64 / h->P;
+  DISPATCH(h, hipLaunchKernelGGL(k_expand<GG>, dim3(nblk(h->v.T, gpb)), dim3(64), 0, (hipStream_t)stream, h->v,
+                                 probs_dev, values_dev));
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int spmcts_search_end(spmcts_arena *h, double temp, int32_t *actions_dev, int8_t *states_dev, float *tree_probs_dev,
+                      double *q_dev, uint8_t *q_f64_dev, uint8_t *recorded_dev, spmcts_stream stream) {
+  if (!h) return fail(-1, "null arena");
+  const int n = h->n_active;
+  if (n <= 0) return 0;
+  DISPATCH(h, hipLaunchKernelGGL(k_search_end<GG>, dim3(nblk(n, 64)), dim3(64), 0, (hipStream_t)stream, h->v, n,
+                                 temp, actions_dev, states_dev, tree_probs_dev, q_dev, q_f64_dev, recorded_dev));
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int spmcts_play_action(spmcts_arena *h, const int32_t *trees_dev, const int32_t *actions_dev, int32_t n,
+                       void *leaves_dev, int32_t *leaf_count_dev, spmcts_stream stream) {
+  if (!h) return fail(-1, "null arena");
+  hipStream_t s = (hipStream_t)stream;
+  if (n > 0)
+    DISPATCH(h, hipLaunchKernelGGL(k_play_action<GG>, dim3(nblk(n, 64)), dim3(64), 0, s, h->v, trees_dev,
+                                   actions_dev, n));
+  LAUNCH_CHECK();
+  return launch_rows(h, leaves_dev, leaf_count_dev, s);
+}
+
+int spmcts_leaf_trees(spmcts_arena *h, int32_t *trees_dev, spmcts_stream stream) {
+  if (!h || !trees_dev) return fail(-1, "null argument");
+  HIP_TRY(hipMemcpyAsync(trees_dev, h->v.row_tree, sizeof(int32_t) * h->v.T, hipMemcpyDeviceToDevice,
+                         (hipStream_t)stream));
+  return 0;
+}
+
+int spmcts_root_stats(spmcts_arena *h, int32_t tree, int32_t *child_n, double *child_w, float *child_p,
+                      int32_t *root_n, double *root_w, int32_t *root_player, int8_t *board) {
+  if (!h) return fail(-1, "null arena");
+  if (tree < 0 || tree >= h->v.T) return fail(-3, "tree out of range");
+  HIP_TRY(hipDeviceSynchronize());
+  const size_t nb = (size_t)tree * h->v.cap * h->P;
+  int32_t root = 0, cb = -1;
+  int8_t rp = 0;
+  uint64_t pos = 0, neg = 0;
+  HIP_TRY(hipMemcpy(&root, h->v.root + tree, 4, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(&cb, h->v.bc + nb + root, 4, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(&rp, h->v.rplayer + tree, 1, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(&pos, h->v.rpos + tree, 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(&neg, h->v.rneg + tree, 8, hipMemcpyDeviceToHost));
+  if (root_n) HIP_TRY(hipMemcpy(root_n, h->v.bn + nb + root, 4, hipMemcpyDeviceToHost));
+  if (root_w) HIP_TRY(hipMemcpy(root_w, h->v.bw + nb + root, 8, hipMemcpyDeviceToHost));
+  if (root_player) *root_player = rp;
+  if (cb >= 0) {
+    const size_t ci = nb + (size_t)cb * h->P;
+    if (child_n) HIP_TRY(hipMemcpy(child_n, h->v.bn + ci, 4 * h->A, hipMemcpyDeviceToHost));
+    if (child_w) HIP_TRY(hipMemcpy(child_w, h->v.bw + ci, 8 * h->A, hipMemcpyDeviceToHost));
+    if (child_p) HIP_TRY(hipMemcpy(child_p, h->v.bp + ci, 4 * h->A, hipMemcpyDeviceToHost));
+  } else {
+    for (int j = 0; j < h->A; ++j) {
+      if (child_n) child_n[j] = 0;
+      if (child_w) child_w[j] = 0.0;
+      if (child_p) child_p[j] = 0.f;
+    }
+  }
+  if (board) {
+    for (int x = 0; x < h->W; ++x)
+      for (int y = 0; y < h->H; ++y) {
+        const uint64_t bit = 1ull << (x * (h->H + 1) + y);
+        board[x * h->H + y] = (pos & bit) ? 1 : ((neg & bit) ? -1 : 0);
+      }
+  }
+  return 0;
+}
+
+int spmcts_games_start(spmcts_arena *h, const int32_t *slots_dev, const float *priors_dev, int32_t n,
+                       spmcts_stream stream) {
+  if (!h) return fail(-1, "null arena");
+  if (h->v.G <= 0) return fail(-4, "arena has no game slots");
+  if (n <= 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  DISPATCH(h, hipLaunchKernelGGL(k_games_start<GG>, dim3(nblk(n, 128)), dim3(128), 0, s, h->v, slots_dev, priors_dev, n));
+  hipLaunchKernelGGL(k_games_bump_id, dim3(1), dim3(1), 0, s, h->v, n);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int spmcts_games_set_limit(spmcts_arena *h, int64_t max_games) {
+  if (!h) return fail(-1, "null arena");
+  HIP_TRY(hipMemcpy(h->v.gcnt + 8, &max_games, 8, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int spmcts_games_begin_ply(spmcts_arena *h, spmcts_stream stream) {
+  if (!h) return fail(-1, "null arena");
+  if (h->v.G <= 0) return fail(-4, "arena has no game slots");
+  h->n_active = h->v.G;
+  DISPATCH(h, hipLaunchKernelGGL(k_games_begin_ply<GG>, dim3(nblk(h->v.G, 128)), dim3(128), 0, (hipStream_t)stream,
+                                 h->v));
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int spmcts_games_end_ply(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_dev, spmcts_stream stream) {
+  if (!h) return fail(-1, "null arena");
+  hipStream_t s = (hipStream_t)stream;
+  DISPATCH(h, hipLaunchKernelGGL(k_games_end_ply<GG>, dim3(nblk(h->v.G, 64)), dim3(64), 0, s, h->v));
+  LAUNCH_CHECK();
+  return launch_rows(h, leaves_dev, leaf_count_dev, s);
+}
+
+int spmcts_games_finish_ply(spmcts_arena *h, int32_t refill, int32_t *out_dev, spmcts_stream stream) {
+  if (!h) return fail(-1, "null arena");
+  hipStream_t s = (hipStream_t)stream;
+  DISPATCH(h, hipLaunchKernelGGL(k_games_finish_scan<GG>, dim3(1), dim3(1024), 0, s, h->v, refill, out_dev));
+  DISPATCH(h, hipLaunchKernelGGL(k_games_finish_apply<GG>, dim3(nblk(h->v.G, 64)), dim3(64), 0, s, h->v));
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int spmcts_export_moves(spmcts_arena *h, int8_t *states_dev, float *tree_probs_dev, double *q_dev, uint8_t *q_f64_dev,
+                        float *z_dev, int64_t *game_dev, int32_t max_records, int32_t *count_dev,
+                        spmcts_stream stream) {
+  if (!h) return fail(-1, "null arena");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_export, dim3(nblk(std::max(1, max_records), 256)), dim3(256), 0, s, h->v, h->A, h->cells,
+                     states_dev, tree_probs_dev, q_dev, q_f64_dev, z_dev, game_dev, max_records, count_dev);
+  hipLaunchKernelGGL(k_export_clear, dim3(1), dim3(1), 0, s, h->v);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int spmcts_games_state(spmcts_arena *h, uint8_t *active, int32_t *ply, uint8_t *swap, int64_t *game_id) {
+  if (!h) return fail(-1, "null arena");
+  HIP_TRY(hipDeviceSynchronize());
+  const size_t G = h->v.G;
+  if (active) HIP_TRY(hipMemcpy(active, h->v.gstate, G, hipMemcpyDeviceToHost));
+  if (ply) HIP_TRY(hipMemcpy(ply, h->v.gply, 4 * G, hipMemcpyDeviceToHost));
+  if (swap) HIP_TRY(hipMemcpy(swap, h->v.gswap, G, hipMemcpyDeviceToHost));
+  if (game_id) HIP_TRY(hipMemcpy(game_id, h->v.gid, 8 * G, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int spmcts_get_counters(spmcts_arena *h, spmcts_counters *out) {
+  if (!h || !out) return fail(-1, "null argument");
+  HIP_TRY(hipDeviceSynchronize());
+  memset(out, 0, sizeof(*out));
+  std::vector<int64_t> c((size_t)h->v.T * C_NCNT);
+  HIP_TRY(hipMemcpy(c.data(), h->v.cnt, c.size() * 8, hipMemcpyDeviceToHost));
+  for (int t = 0; t < h->v.T; ++t) {
+    const int64_t *ct = c.data() + (size_t)t * C_NCNT;
+    out->sims += ct[C_SIMS];
+    out->nn_leaves += ct[C_NN];
+    out->terminal_leaves += ct[C_TERM];
+    out->depth_sum += ct[C_DEPTH];
+    out->set_node_expansions += ct[C_SETNODE];
+    out->moves += ct[C_MOVES];
+  }
+  std::vector<int32_t> used(h->v.T);
+  HIP_TRY(hipMemcpy(used.data(), h->v.used, 4 * used.size(), hipMemcpyDeviceToHost));
+  for (int32_t u : used) out->blocks_in_use_max = std::max<int64_t>(out->blocks_in_use_max, u);
+  int64_t g[16];
+  HIP_TRY(hipMemcpy(g, h->v.gcnt, sizeof(g), hipMemcpyDeviceToHost));
+  out->games_finished = g[0];
+  for (int k = 0; k < 6; ++k) out->results[k / 3][k % 3] = g[1 + k];
+  out->positions_exported = g[9];
+  HIP_TRY(hipMemcpy(&out->error_flags, h->v.err, 4, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int spmcts_check(spmcts_arena *h) {
+  if (!h) return fail(-1, "null arena");
+  HIP_TRY(hipDeviceSynchronize());
+  uint32_t e = 0;
+  HIP_TRY(hipMemcpy(&e, h->v.err, 4, hipMemcpyDeviceToHost));
+  if (e) {
+    char buf[128];
+    snprintf(buf, sizeof(buf), "device error flags 0x%x", e);
+    return fail(-5, buf);
+  }
+  return 0;
+}
+
+int spmcts_env_step(int32_t game, int32_t width, int32_t height, const int8_t *boards_dev, const int32_t *actions_dev,
+                    const int8_t *players_dev, const uint8_t *over_dev, int32_t n, int8_t *out_boards_dev,
+                    int8_t *reward_dev, uint8_t *done_dev, int8_t *status_dev, uint8_t *valid_dev,
+                    spmcts_stream stream) {
+  if (n <= 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (game == SPMCTS_CONNECT4 && width == 7 && height == 6)
+    hipLaunchKernelGGL(k_env_step<C4>, dim3(nblk(n, 256)), dim3(256), 0, s, boards_dev, actions_dev, players_dev,
+                       over_dev, n, out_boards_dev, reward_dev, done_dev, status_dev, valid_dev);
+  else if (game == SPMCTS_TICTACTOE && width == 3 && height == 3)
+    hipLaunchKernelGGL(k_env_step<TTT>, dim3(nblk(n, 256)), dim3(256), 0, s, boards_dev, actions_dev, players_dev,
+                       over_dev, n, out_boards_dev, reward_dev, done_dev, status_dev, valid_dev);
+  else
+    return fail(-2, "unsupported game/board size");
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int spmcts_env_step_host(int32_t game, int32_t width, int32_t height, int8_t *board, int32_t action, int32_t player,
+                         int32_t *reward, int32_t *done) {
+  if (game == SPMCTS_CONNECT4 && width == 7 && height == 6) {
+    if (action < 0 || action >= C4::A) return fail(-3, "action out of range");
+    return env_step_host_t<C4>(board, action, player, reward, done);
+  }
+  if (game == SPMCTS_TICTACTOE && width == 3 && height == 3) {
+    if (action < 0 || action >= TTT::A) return fail(-3, "action out of range");
+    return env_step_host_t<TTT>(board, action, player, reward, done);
+  }
+  return fail(-2, "unsupported game/board size");
+}
+
+int spmcts_valid_moves_host(int32_t game, int32_t width, int32_t height, const int8_t *board, uint8_t *valid) {
+  if (game == SPMCTS_CONNECT4 && width == 7 && height == 6) {
+    const uint32_t m = legal_mask<C4>(from_cells<C4>(board));
+    for (int a = 0; a < C4::A; ++a) valid[a] = (m >> a) & 1u;
+    return 0;
+  }
+  if (game == SPMCTS_TICTACTOE && width == 3 && height == 3) {
+    const uint32_t m = legal_mask<TTT>(from_cells<TTT>(board));
+    for (int a = 0; a < TTT::A; ++a) valid[a] = (m >> a) & 1u;
+    return 0;
+  }
+  return fail(-2, "unsupported game/board size");
+}
+
+int spmcts_table_net(int32_t game, int32_t width, int32_t height, const void *leaves_dev, int32_t leaf_format,
+                     int32_t leaf_layout, int32_t n, uint64_t salt, const uint64_t *salts_dev, float *probs_dev,
+                     float *values_dev, spmcts_stream stream) {
+  if (n <= 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (game == SPMCTS_CONNECT4 && width == 7 && height == 6)
+    hipLaunchKernelGGL(k_table_net<C4>, dim3(nblk(n, 128)), dim3(128), 0, s, leaves_dev, leaf_format, leaf_layout, n,
+                       salt, salts_dev, probs_dev, values_dev);
+  else if (game == SPMCTS_TICTACTOE && width == 3 && height == 3)
+    hipLaunchKernelGGL(k_table_net<TTT>, dim3(nblk(n, 128)), dim3(128), 0, s, leaves_dev, leaf_format, leaf_layout,
+                       n, salt, salts_dev, probs_dev, values_dev);
+  else
+    return fail(-2, "unsupported game/board size");
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int spmcts_copy_probe(const void *src_dev, void *dst_dev, uint64_t bytes, spmcts_stream stream) {
+  const size_t n4 = bytes / 16;
+  hipLaunchKernelGGL(k_copy_probe, dim3(4096), dim3(256), 0, (hipStream_t)stream, (const float4 *)src_dev,
+                     (float4 *)dst_dev, n4);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,145 @@
+"""Multi-GPU self-play: one process per GPU, games sharded, RCCL only at episode end.
+
+The reference's only parallelism is CPU processes exchanging every leaf over
+multiprocessing queues (games/algos/self_play_parallel.py:95-171,
+rl_utils/queues.py).  Games are independent units (they share only frozen
+weights within an epoch), so here every rank owns its own arena of game slots
+and its own Philox subsequences (subsequence0 = rank * n_trees) and the data
+path has no collective.  The exchange steps are the ones the reference has:
+
+  * episode statistics (games finished, wins/draws/losses by side) are summed
+    over ranks — `all_reduce(SUM)` of an int64[8] per ply
+    (self_play_parallel.py:302-327 parse_results, result_queue);
+  * finished games' Move records go to the replay owner on rank 0
+    (memory_queue -> UpdateWorker -> Memory, mcts.py:225-232,
+    updateworker.py:119-125): all_gather of per-rank counts, then of the
+    records packed into fixed-size byte rows;
+  * weights are broadcast from rank 0 at epoch boundaries (the reference's
+    checkpoint reload, selfplayworker.py:109-114).
+
+backend "nccl" is RCCL on ROCm (xGMI between the GPUs of a node); the same
+code runs on "gloo" for CPU tests.
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+STAT_FIELDS = ("games", "moves", "first_w", "first_d", "first_l", "second_w", "second_d", "second_l")
+
+
+def env_rank():
+    return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("LOCAL_RANK", 0))
+
+
+def init_from_env(backend=None):
+    """Initialise torch.distributed from torchrun's environment (no-op for world size 1)."""
+    rank, world, local = env_rank()
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        kw = {}
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            kw["device_id"] = torch.device("cuda", local)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
+    elif torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    return rank, world, local
+
+
+def is_distributed():
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def _comm_device():
+    return torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+
+
+def barrier():
+    if is_distributed():
+        if dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+def all_reduce_stats(stats):
+    """Sum an int64 stats vector over ranks (returns a CPU tensor)."""
+    t = torch.as_tensor(stats, dtype=torch.int64)
+    if not is_distributed():
+        return t.cpu()
+    t = t.to(_comm_device())
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.cpu()
+
+
+def all_reduce_max(value):
+    t = torch.tensor([float(value)], dtype=torch.float64)
+    if not is_distributed():
+        return float(t[0])
+    t = t.to(_comm_device())
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.cpu()[0])
+
+
+# ---------------------------------------------------------------- Move records
+_FIELDS = (("state", torch.int8), ("tree_probs", torch.float32), ("q", torch.float64), ("q_f64", torch.uint8),
+           ("z", torch.float32), ("game", torch.int64))
+
+
+def pack_moves(moves):
+    """Dict of per-record tensors -> uint8 [n, row_bytes] (one row per Move)."""
+    n = moves["z"].shape[0]
+    cols = []
+    for name, dt in _FIELDS:
+        t = moves[name].to(dt).reshape(n, -1).contiguous()
+        cols.append(t.view(torch.uint8).reshape(n, -1))
+    return torch.cat(cols, dim=1)
+
+
+def unpack_moves(rows, cells, n_actions):
+    widths = {"state": cells, "tree_probs": 4 * n_actions, "q": 8, "q_f64": 1, "z": 4, "game": 8}
+    out, off = {}, 0
+    for name, dt in _FIELDS:
+        w = widths[name]
+        chunk = rows[:, off:off + w].contiguous()
+        t = chunk.view(dt)
+        out[name] = t if name in ("state", "tree_probs") else t.reshape(-1)
+        off += w
+    return out
+
+
+def gather_moves(moves, cells, n_actions, dst=0):
+    """Gather every rank's Move records to rank `dst` (others get None)."""
+    if not is_distributed():
+        return moves
+    dev = _comm_device()
+    rows = pack_moves(moves).to(dev)
+    n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=dev)
+    counts = [torch.zeros_like(n) for _ in range(dist.get_world_size())]
+    dist.all_gather(counts, n)
+    counts = [int(c.item()) for c in counts]
+    width = rows.shape[1]
+    mx = max(max(counts), 1)
+    pad = torch.zeros((mx, width), dtype=torch.uint8, device=dev)
+    pad[: rows.shape[0]] = rows
+    bufs = [torch.zeros_like(pad) for _ in counts]
+    dist.all_gather(bufs, pad)
+    if dist.get_rank() != dst:
+        return None
+    allrows = torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0).cpu()
+    return unpack_moves(allrows, cells, n_actions)
+
+
+def broadcast_state_dict(module, src=0):
+    """Epoch-boundary weight refresh from the trainer rank (in place)."""
+    if not is_distributed():
+        return
+    dev = _comm_device()
+    for t in list(module.state_dict().values()):
+        buf = t.detach().to(dev)
+        dist.broadcast(buf, src=src)
+        t.copy_(buf.to(t.device))

@@ -1,0 +1,119 @@
+"""CPU: the oracle (numpy restatement) reproduces the reference's own outputs (golden fixtures)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle.envs import Connect4Env, GameOver, TicTacToeEnv
+from oracle.mcts import NumpyRNG, OracleTree, RecordingRNG, TapeRNG
+from oracle.selfplay import play_episode
+from oracle.table_net import TableNet
+from tests.parity_helpers import A_OF, load_json
+
+pytestmark = pytest.mark.filterwarnings("ignore::DeprecationWarning")
+
+
+def _kat(golden_dir, name):
+    return dict(np.load(os.path.join(golden_dir, f"env_kat_{name}.npz")))
+
+
+@pytest.mark.parametrize("name,Env", [("c4", Connect4Env), ("ttt", TicTacToeEnv)])
+def test_env_kat(golden_dir, name, Env):
+    k = _kat(golden_dir, name)
+    for i in range(len(k["action"])):
+        e = Env()
+        e.set_state(k["before"][i].astype(np.int64))
+        if k["status"][i] == 2:
+            e.episode_over = True
+        try:
+            s, r, d, _ = e.step(int(k["action"][i]), int(k["player"][i]))
+            st = 0
+        except ValueError:
+            st, s = 1, e.board
+        except GameOver:
+            st, s = 2, e.board
+        assert st == k["status"][i], i
+        assert np.array_equal(s, k["after"][i]), i
+        if st == 0:
+            assert r == k["reward"][i] and d == k["done"][i], i
+            assert np.array_equal(e.valid_moves(), k["valid"][i]), i
+
+
+def test_env_kat_covers_all_win_directions(golden_dir):
+    """The C4 KAT holds wins along rows, columns and both diagonals, and full-board draws."""
+    k = _kat(golden_dir, "c4")
+    seen = set()
+    for i in np.nonzero((k["reward"] == 1) & (k["status"] == 0))[0]:
+        b, p = k["after"][i].astype(int) * k["player"][i], None
+        for name, (dx, dy) in {"h": (1, 0), "v": (0, 1), "d1": (1, 1), "d2": (1, -1)}.items():
+            for x in range(7):
+                for y in range(6):
+                    if all(0 <= x + j * dx < 7 and 0 <= y + j * dy < 6 and b[x + j * dx, y + j * dy] == 1
+                           for j in range(4)):
+                        seen.add(name)
+    assert seen == {"h", "v", "d1", "d2"}
+    draws = (k["done"] & (k["reward"] == 0) & (k["status"] == 0))
+    assert draws.any()
+    assert (k["status"] == 1).any() and (k["status"] == 2).any()
+
+
+@pytest.mark.parametrize("idx", range(0, 182, 1))
+def test_mcts_search_matches_reference(idx):
+    c = load_json("mcts_search.json")[idx]
+    net = TableNet(A_OF[c["game"]], c["salt"])
+    np.random.seed(c["seed"])
+    t = OracleTree(c["game"], net, NumpyRNG(), c["sims"], strong_play=c["strong_play"])
+    for a in c["opening"]:
+        t.play_action(a)
+    assert t.root.player == c["root_player"]
+    a = t.move()
+    st = t.root_stats()
+    rec = t.temp_memory[-1]
+    assert a == c["action"]
+    assert st["child_n"] == c["child_n"] and st["child_w"] == c["child_w"]
+    assert st["root_n"] == c["root_n"] and st["root_w"] == c["root_w"]
+    assert rec["state"].reshape(-1).tolist() == c["state"]
+    assert rec["tree_probs"].astype(float).tolist() == c["tree_probs"]
+    assert float(rec["q"]) == c["q"]
+    assert net.calls == c["net_calls"]
+
+
+def test_tape_replay_equals_numpy_stream():
+    """Recording the numpy stream and replaying it as a tape gives the identical search."""
+    c = load_json("mcts_search.json")[30]
+    A = A_OF[c["game"]]
+    np.random.seed(c["seed"])
+    rec = RecordingRNG(NumpyRNG())
+    t1 = OracleTree(c["game"], TableNet(A, c["salt"]), rec, c["sims"])
+    for a in c["opening"]:
+        t1.play_action(a)
+    a1 = t1.move()
+    t2 = OracleTree(c["game"], TableNet(A, c["salt"]), TapeRNG(rec.tape), c["sims"])
+    for a in c["opening"]:
+        t2.play_action(a)
+    a2 = t2.move()
+    assert a1 == a2 and t1.root_stats() == t2.root_stats()
+
+
+@pytest.mark.parametrize("idx", range(48))
+def test_selfplay_games_match_reference(idx):
+    g = load_json("selfplay_games.json")[idx]
+    A = A_OF[g["game"]]
+    net_p = TableNet(A, g["salt_policy"])
+    net_o = net_p if not g["evaluate"] else TableNet(A, g["salt_opponent"])
+    np.random.seed(g["seed"])
+    rng = NumpyRNG()
+    r, moves, log, _ = play_episode(g["game"], net_p, net_o, rng, rng, g["sims"], swap_sides=g["swap_sides"],
+                                    update=not g["evaluate"], evaluate=g["evaluate"])
+    assert r == g["result"]
+    assert len(log) == len(g["plies"])
+    for L, P in zip(log, g["plies"]):
+        for k in ("tree", "action", "child_n", "child_w", "root_n", "root_w", "tree_probs", "q"):
+            assert L[k] == P[k], k
+    assert len(moves) == len(g["moves"])
+    for m, M in zip(moves, g["moves"]):
+        assert m["state"].reshape(-1).tolist() == M["state"]
+        assert float(m["actual_val"]) == M["actual_val"]
+        assert m["tree_probs"].astype(float).tolist() == M["tree_probs"]
+        assert float(m["q"]) == M["q"]
