@@ -207,6 +207,17 @@ int spmcts_valid_moves_host(int32_t game, int32_t width, int32_t height, const i
 int spmcts_table_net(int32_t game, int32_t width, int32_t height, const void *leaves_dev, int32_t leaf_format,
                      int32_t leaf_layout, int32_t n, uint64_t salt, const uint64_t *salts_dev /* [n] or NULL */,
                      float *probs_dev, float *values_dev, spmcts_stream stream);
+/* Fused residual-tower trunk for leaf evaluation (games/general/modules.py:43-107
+ * with BatchNorm folded): stem conv3x3 + num_blocks BasicBlocks + the policy/value
+ * 1x1 head convs, bias + ReLU (+ residual) fused, activations resident in LDS,
+ * bf16 MFMA with fp32 accumulation.  planes_dev: bf16 [batch][W][H][3] (NHWC
+ * leaf rows); features_dev: bf16 [batch][W*H][channels/2] (policy | value head
+ * channels, cell-major).  Packed weight/bias layout: csrc/tower.hip.  Instantiated
+ * for 7x6 and 3x3 boards with channels 128 or 256. */
+int spmcts_tower_forward(int32_t width, int32_t height, int32_t channels, int32_t n_blocks, const void *planes_dev,
+                         int32_t batch, const void *weights_dev, const float *bias_dev, void *features_dev,
+                         spmcts_stream stream);
+int spmcts_tower_supported(int32_t width, int32_t height, int32_t channels);
 /* Memory-roofline helper: device copy bandwidth probe (bytes each way). */
 int spmcts_copy_probe(const void *src_dev, void *dst_dev, uint64_t bytes, spmcts_stream stream);
 

@@ -1,0 +1,46 @@
+"""Micro-benchmark: fused HIP tower vs PyTorch bf16 path for the leaf evaluator (ResNet-128x20, 4096 boards)."""
+import argparse
+import json
+import sys
+import os
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from bench import resnet_flops_per_leaf
+from self_play_reinforcement_learning_amd.evaluator import HipTowerEvaluator, TowerEvaluator
+from self_play_reinforcement_learning_amd.modules import ResidualTower, planes_from_boards
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--batch", type=int, default=4096)
+ap.add_argument("--ff", type=int, default=32)
+ap.add_argument("--blocks", type=int, default=20)
+ap.add_argument("--iters", type=int, default=20)
+args = ap.parse_args()
+torch.manual_seed(0)
+net = ResidualTower(7, 6, 7, num_blocks=args.blocks, filter_factor=args.ff).cuda().eval()
+b = torch.randint(-1, 2, (args.batch, 7, 6))
+x = planes_from_boards(b, 7, 6).cuda().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+fl = resnet_flops_per_leaf(7, 6, 7, args.ff, args.blocks) * args.batch
+out = {}
+for name, ev in (("hip", HipTowerEvaluator(net)), ("torch_bf16", TowerEvaluator(net, dtype=torch.bfloat16))):
+    for _ in range(3):
+        ev(x)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(args.iters):
+        ev(x)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / args.iters
+    out[name] = dict(ms=ms, tflops=fl / ms / 1e9)
+    if name == "hip":
+        e0.record()
+        for _ in range(args.iters):
+            ev.trunk(x.permute(0, 2, 3, 1))
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / args.iters
+        out["hip_trunk_only"] = dict(ms=ms, tflops=fl / ms / 1e9)
+print(json.dumps(dict(batch=args.batch, ff=args.ff, blocks=args.blocks, **out)))

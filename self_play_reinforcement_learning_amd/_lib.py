@@ -111,6 +111,8 @@ _SIGS = {
     "spmcts_table_net": [_I32, _I32, _I32, _P, _I32, _I32, _I32, _U64, _P, _P, _P, _P],
     "spmcts_leaf_trees": [_P, _P, _P],
     "spmcts_copy_probe": [_P, _P, _U64, _P],
+    "spmcts_tower_forward": [_I32, _I32, _I32, _I32, _P, _I32, _P, _P, _P, _P],
+    "spmcts_tower_supported": [_I32, _I32, _I32],
 }
 
 # every symbol the header declares (tests check the .so exports exactly these)

@@ -1,0 +1,278 @@
+// tower.hip — fused residual-tower inference for the leaf evaluator (gfx950, bf16 MFMA).
+//
+// Evaluates the trunk of games/general/modules.py ResidualTower (stem conv3x3 +
+// BN + ReLU, num_blocks x BasicBlock, and the two 1x1 head convs + BN + ReLU) for a
+// batch of boards in ONE launch.  BatchNorm is folded into the conv weights/bias
+// on the host (eval-mode statistics), so every layer is conv + bias (+ residual)
+// + ReLU.
+//
+// One workgroup owns BOARDS whole boards (ROWS = 256 or 128 cell rows, NHWC) and
+// keeps their activations resident in LDS for the whole tower: two ping-pong
+// buffers X / Y of (ROWS + 1) rows x (C*2 + 16) bytes (the +16 pad makes the
+// 16-byte MFMA operand reads bank-conflict free; row ROWS is all zeros and stands
+// for the conv's zero padding).  A 3x3 conv is an implicit GEMM
+//     out[c_out][cell] = sum_{tap, c_in} W[c_out][tap][c_in] * act[nbr(cell, tap)][c_in]
+// on v_mfma_f32_32x32x16_bf16: A = weights (32 output channels x 16 k), streamed
+// from global memory (L2/MALL resident, pre-swizzled so every wave reads one
+// contiguous 1 KiB fragment per k-step), B = activations (16 k x 32 cells) read
+// from LDS with a per-(tap, cell) neighbour table.  Each wave owns C/4 output
+// channels for all ROWS cells; fp32 accumulators, bf16 activations between
+// layers (as the bf16 PyTorch path).  HBM traffic per board: 42 x 3 input planes
+// + 42 x 64 head features, i.e. the activations never leave the CU.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "spmcts.h"
+
+namespace tower {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+
+template <int C_, int ROWS_, int W_, int H_>
+struct Cfg {
+  static constexpr int C = C_, ROWS = ROWS_, W = W_, H = H_;
+  static constexpr int CELLS = W * H;
+  static constexpr int BOARDS = ROWS / CELLS;
+  static constexpr int VROWS = BOARDS * CELLS;
+  static constexpr int RS = C * 2 + 16;  // bytes per LDS row
+  static constexpr int ZROW = ROWS;
+  static constexpr int NT = ROWS / 32;  // 32-cell tiles
+  static constexpr int MT = C / 128;    // 32-channel tiles per wave (4 waves)
+  static constexpr int BUF = (ROWS + 1) * RS;
+  static constexpr int LDS = 2 * BUF + 9 * ROWS * 2;
+  static constexpr int HEAD = C / 2;  // policy filter_factor | value filter_factor channels (filter_factor = C/4)
+  static constexpr int HCT = HEAD / 32;  // head channel tiles
+  static_assert(MT * NT == 8, "tile plan assumes 8 accumulator tiles per wave");
+  static_assert(BOARDS >= 1, "board larger than a tile");
+  static_assert(LDS <= 163840, "LDS budget");
+};
+
+__device__ __forceinline__ bf16x8 lds_b128(const char *p) { return *(const bf16x8 *)p; }
+
+// One conv layer over the resident tile: src (LDS) -> dst (LDS), optional residual (LDS, == dst).
+// KK = input channels / 16 (k-steps per tap), TAPS = 9 (3x3) or 1 (1x1, centre only).
+template <class K, int KK, int TAPS, bool RESID>
+__device__ __forceinline__ void conv_layer(const char *src, char *dst, const int16_t *tapt, const bf16x8 *w,
+                                           const float *bias, int wave, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+  f32x16 acc[K::MT][K::NT];
+#pragma unroll
+  for (int m = 0; m < K::MT; ++m)
+#pragma unroll
+    for (int t = 0; t < K::NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[m][t][i] = 0.f;
+
+  // weight fragment index of (ctile, tap, kk): ((ct * TAPS + tap) * KK + kk) * 64 + lane
+  constexpr int STEPS = TAPS * KK;
+  bf16x8 a_cur[K::MT], a_nxt[K::MT];
+#pragma unroll
+  for (int m = 0; m < K::MT; ++m) a_cur[m] = w[((size_t)(wave * K::MT + m) * STEPS) * 64 + lane];
+
+  for (int tap = 0; tap < TAPS; ++tap) {
+    int rows[K::NT];
+    const int tap_id = TAPS == 1 ? 4 : tap;
+#pragma unroll
+    for (int t = 0; t < K::NT; ++t) rows[t] = tapt[tap_id * K::ROWS + t * 32 + r];
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      const int s = tap * KK + kk;
+      if (s + 1 < STEPS) {
+#pragma unroll
+        for (int m = 0; m < K::MT; ++m)
+          a_nxt[m] = w[((size_t)(wave * K::MT + m) * STEPS + s + 1) * 64 + lane];
+      }
+      const int koff = (kk * 16 + 8 * h) * 2;
+#pragma unroll
+      for (int t = 0; t < K::NT; ++t) {
+        const bf16x8 b = lds_b128(src + rows[t] * K::RS + koff);
+#pragma unroll
+        for (int m = 0; m < K::MT; ++m) acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_cur[m], b, acc[m][t], 0, 0, 0);
+      }
+#pragma unroll
+      for (int m = 0; m < K::MT; ++m) a_cur[m] = a_nxt[m];
+    }
+  }
+  // epilogue: bias (+ residual) + ReLU -> bf16 rows of dst
+#pragma unroll
+  for (int m = 0; m < K::MT; ++m) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int ch = (wave * K::MT + m) * 32 + 8 * g + 4 * h;
+      const float4 bv = *(const float4 *)(bias + ch);
+#pragma unroll
+      for (int t = 0; t < K::NT; ++t) {
+        const int cell = t * 32 + r;
+        char *p = dst + cell * K::RS + ch * 2;
+        float v0 = acc[m][t][4 * g + 0] + bv.x, v1 = acc[m][t][4 * g + 1] + bv.y;
+        float v2 = acc[m][t][4 * g + 2] + bv.z, v3 = acc[m][t][4 * g + 3] + bv.w;
+        if (RESID) {
+          const bf16x4 x = *(const bf16x4 *)p;
+          v0 += (float)x[0];
+          v1 += (float)x[1];
+          v2 += (float)x[2];
+          v3 += (float)x[3];
+        }
+        bf16x4 o;
+        o[0] = (__bf16)fmaxf(v0, 0.f);
+        o[1] = (__bf16)fmaxf(v1, 0.f);
+        o[2] = (__bf16)fmaxf(v2, 0.f);
+        o[3] = (__bf16)fmaxf(v3, 0.f);
+        *(bf16x4 *)p = o;
+      }
+    }
+  }
+}
+
+// 1x1 head convs (C -> C/4 policy | C/4 value) + bias + ReLU, to global features
+// [board][cell][C/2] (cell-major: the order the NHWC-reordered linear heads expect).
+template <class K>
+__device__ __forceinline__ void head_layer(const char *src, const bf16x8 *w, const float *bias, __bf16 *out,
+                                           int board0, int batch, int wave, int lane) {
+  constexpr int KK = K::C / 16;
+  constexpr int GROUPS = 4 / K::HCT;       // waves sharing one head channel tile
+  constexpr int TPW = K::NT / GROUPS;      // cell tiles per wave
+  static_assert(K::HCT * GROUPS == 4 && TPW * GROUPS == K::NT, "head tile plan");
+  const int r = lane & 31, h = lane >> 5;
+  const int ct = wave % K::HCT;
+  const int t0 = (wave / K::HCT) * TPW;
+  f32x16 acc[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+#pragma unroll 4
+  for (int kk = 0; kk < KK; ++kk) {
+    const bf16x8 a = w[((size_t)ct * KK + kk) * 64 + lane];
+    const int koff = (kk * 16 + 8 * h) * 2;
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      const int cell = (t0 + t) * 32 + r;
+      const bf16x8 b = lds_b128(src + cell * K::RS + koff);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[t], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int ch = ct * 32 + 8 * g + 4 * h;
+    const float4 bv = *(const float4 *)(bias + ch);
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      const int row = (t0 + t) * 32 + r;
+      if (row >= K::VROWS) continue;
+      const int board = board0 + row / K::CELLS;
+      if (board >= batch) continue;
+      const int cell = row % K::CELLS;
+      bf16x4 o;
+      o[0] = (__bf16)fmaxf(acc[t][4 * g + 0] + bv.x, 0.f);
+      o[1] = (__bf16)fmaxf(acc[t][4 * g + 1] + bv.y, 0.f);
+      o[2] = (__bf16)fmaxf(acc[t][4 * g + 2] + bv.z, 0.f);
+      o[3] = (__bf16)fmaxf(acc[t][4 * g + 3] + bv.w, 0.f);
+      *(bf16x4 *)(out + ((size_t)board * K::CELLS + cell) * K::HEAD + ch) = o;
+    }
+  }
+}
+
+// Packed weight blob (bf16x8 units) and bias blob (floats), in layer order:
+//   stem   [C/32][9][1][64 lanes]      k = 16 input channels (3 planes + 13 zero)
+//   block  2 x [C/32][9][C/16][64]      per BasicBlock (conv1, conv2)
+//   head   [C/64][1][C/16][64]          policy C/4 | value C/4 output channels
+// lane l of fragment (ct, tap, kk) holds W[ct*32 + (l & 31)][tap][kk*16 + 8*(l >> 5) + j], j = 0..7.
+// bias: stem C, blocks 2*C each, head C/2.
+template <class K>
+__global__ __launch_bounds__(256) void k_tower(const __bf16 *planes, int batch, int n_blocks, const bf16x8 *wpk,
+                                               const float *bias, __bf16 *out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char *X = smem;
+  char *Y = smem + K::BUF;
+  int16_t *tapt = (int16_t *)(smem + 2 * K::BUF);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int board0 = blockIdx.x * K::BOARDS;
+
+  // neighbour table: tapt[tap][row] = source row of (row's cell shifted by tap) or ZROW
+  for (int i = tid; i < 9 * K::ROWS; i += 256) {
+    const int tap = i / K::ROWS, row = i % K::ROWS;
+    int src = K::ZROW;
+    if (row < K::VROWS) {
+      const int cell = row % K::CELLS, x = cell / K::H, y = cell % K::H;
+      const int nx = x + tap / 3 - 1, ny = y + tap % 3 - 1;
+      if (nx >= 0 && nx < K::W && ny >= 0 && ny < K::H) src = row - cell + nx * K::H + ny;
+    }
+    tapt[i] = (int16_t)src;
+  }
+  // zero rows + stem input: Y rows hold 16 channels (3 planes, 13 zeros)
+  for (int i = tid; i < K::RS / 4; i += 256) {
+    ((uint32_t *)(X + K::ZROW * K::RS))[i] = 0u;
+    ((uint32_t *)(Y + K::ZROW * K::RS))[i] = 0u;
+  }
+  for (int row = tid; row < K::ROWS; row += 256) {
+    const int board = board0 + row / K::CELLS;
+    __bf16 *dst = (__bf16 *)(Y + row * K::RS);
+    const bool ok = row < K::VROWS && board < batch;
+    const size_t src = ((size_t)board * K::CELLS + row % K::CELLS) * 3;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) dst[c] = (ok && c < 3) ? planes[src + c] : (__bf16)0.f;
+  }
+  __syncthreads();
+
+  const bf16x8 *w = wpk;
+  const float *b = bias;
+  conv_layer<K, 1, 9, false>(Y, X, tapt, w, b, wave, lane);
+  w += (size_t)K::C / 32 * 9 * 1 * 64;
+  b += K::C;
+  __syncthreads();
+  for (int blk = 0; blk < n_blocks; ++blk) {
+    conv_layer<K, K::C / 16, 9, false>(X, Y, tapt, w, b, wave, lane);
+    w += (size_t)K::C / 32 * 9 * (K::C / 16) * 64;
+    b += K::C;
+    __syncthreads();
+    conv_layer<K, K::C / 16, 9, true>(Y, X, tapt, w, b, wave, lane);
+    w += (size_t)K::C / 32 * 9 * (K::C / 16) * 64;
+    b += K::C;
+    __syncthreads();
+  }
+  head_layer<K>(X, w, b, out, board0, batch, wave, lane);
+}
+
+template <class K>
+static int launch(const void *planes, int batch, int n_blocks, const void *w, const float *b, void *out,
+                  hipStream_t s) {
+  const int grid = (batch + K::BOARDS - 1) / K::BOARDS;
+  if (grid <= 0) return 0;
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute((const void *)k_tower<K>, hipFuncAttributeMaxDynamicSharedMemorySize, K::LDS) !=
+        hipSuccess)
+      return -10;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(k_tower<K>, dim3(grid), dim3(256), K::LDS, s, (const __bf16 *)planes, batch, n_blocks,
+                     (const bf16x8 *)w, b, (__bf16 *)out);
+  return hipGetLastError() == hipSuccess ? 0 : -11;
+}
+
+}  // namespace tower
+
+extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t channels, int32_t n_blocks,
+                                    const void *planes_dev, int32_t batch, const void *weights_dev,
+                                    const float *bias_dev, void *features_dev, spmcts_stream stream) {
+  using namespace tower;
+  hipStream_t s = (hipStream_t)stream;
+  if (n_blocks < 0 || batch < 0) return -3;
+  if (width == 7 && height == 6 && channels == 128)
+    return launch<Cfg<128, 256, 7, 6>>(planes_dev, batch, n_blocks, weights_dev, bias_dev, features_dev, s);
+  if (width == 7 && height == 6 && channels == 256)
+    return launch<Cfg<256, 128, 7, 6>>(planes_dev, batch, n_blocks, weights_dev, bias_dev, features_dev, s);
+  if (width == 3 && height == 3 && channels == 128)
+    return launch<Cfg<128, 256, 3, 3>>(planes_dev, batch, n_blocks, weights_dev, bias_dev, features_dev, s);
+  if (width == 3 && height == 3 && channels == 256)
+    return launch<Cfg<256, 128, 3, 3>>(planes_dev, batch, n_blocks, weights_dev, bias_dev, features_dev, s);
+  return -2;
+}
+
+extern "C" int spmcts_tower_supported(int32_t width, int32_t height, int32_t channels) {
+  return ((width == 7 && height == 6) || (width == 3 && height == 3)) && (channels == 128 || channels == 256);
+}

@@ -141,13 +141,18 @@ class CallableEvaluator(Evaluator):
         return torch.as_tensor(probs).to(leaves.device), torch.as_tensor(values).to(leaves.device)
 
 
-def make_evaluator(network, game, device=None, dtype=torch.bfloat16, leaf_layout="nhwc"):
+def make_evaluator(network, game, device=None, dtype=torch.bfloat16, leaf_layout="nhwc", backend="auto"):
+    """backend: "auto" (fused HIP trunk when instantiated for the net, else torch), "hip", "torch"."""
     _, W, H, A = GAMES[game]
     if isinstance(network, Evaluator):
         return network
     if isinstance(network, DeviceTableNet):
         return TableEvaluator(network)
     if isinstance(network, nn.Module) and hasattr(network, "residual_blocks") and hasattr(network, "conv_policy"):
+        if device is not None:
+            network.to(device)
+        if backend == "hip" or (backend == "auto" and dtype == torch.bfloat16 and HipTowerEvaluator.supported(network)):
+            return HipTowerEvaluator(network, device=device)
         return TowerEvaluator(network, dtype=dtype, leaf_layout=leaf_layout, device=device)
     if isinstance(network, nn.Module):
         if device is not None:
@@ -157,3 +162,117 @@ def make_evaluator(network, game, device=None, dtype=torch.bfloat16, leaf_layout
     if callable(network):
         return CallableEvaluator(network, A)
     raise TypeError(f"cannot evaluate leaves with {type(network).__name__}")
+
+
+# ----------------------------------------------------------------------------- fused HIP tower
+def _pack_conv(w, cin_pad=None):
+    """[Cout][Cin][kh][kw] fp -> bf16 fragments [Cout/32][taps][Cin/16][64 lanes][8] (csrc/tower.hip)."""
+    cout, cin, kh, kw = w.shape
+    if cin_pad is not None and cin_pad > cin:
+        w = torch.cat([w, torch.zeros(cout, cin_pad - cin, kh, kw, dtype=w.dtype, device=w.device)], 1)
+        cin = cin_pad
+    taps = kh * kw
+    w = w.permute(0, 2, 3, 1).reshape(cout, taps, cin)               # [o][tap][c], tap = i*3 + j
+    w = w.reshape(cout // 32, 32, taps, cin // 16, 2, 8)             # o = ct*32 + r ; c = kk*16 + h*8 + j
+    w = w.permute(0, 2, 3, 4, 1, 5)                                  # [ct][tap][kk][h][r][j] -> lane = h*32 + r
+    return w.reshape(-1).to(torch.bfloat16)
+
+
+class HipTowerEvaluator(Evaluator):
+    """ResidualTower leaf evaluation on the fused HIP trunk kernel (csrc/tower.hip).
+
+    The stem, every BasicBlock and the two 1x1 head convs run in one launch with
+    the activations resident in LDS; the three small linear heads (policy
+    1344->A + softmax, value 1344->8ff->1 + tanh) run as bf16 GEMMs in torch.
+    """
+
+    leaf_format = "bf16"
+    leaf_layout = "nhwc"
+
+    def __init__(self, tower, device=None):
+        from . import _lib
+
+        self._lib = _lib
+        self.tower = tower
+        self.device = device
+        self.C = 4 * tower.filter_factor
+        self.W, self.H, self.A = tower.width, tower.height, tower.action_size
+        if not _lib.lib().spmcts_tower_supported(self.W, self.H, self.C):
+            raise ValueError(f"fused tower not instantiated for {self.W}x{self.H} boards, {self.C} channels")
+        self.refresh()
+
+    @staticmethod
+    def supported(tower):
+        from . import _lib
+
+        C = 4 * getattr(tower, "filter_factor", 0)
+        return bool(_lib.lib().spmcts_tower_supported(tower.width, tower.height, C))
+
+    @torch.no_grad()
+    def refresh(self):
+        t = self.tower
+        dev = self.device if self.device is not None else next(t.parameters()).device
+        was = t.training
+        t.eval()
+        fold = InferenceTower._fold
+        ws, bs = [], []
+        w, b = fold(t.conv1, t.bn1)
+        ws.append(_pack_conv(w, cin_pad=16))
+        bs.append(b)
+        for blk in t.residual_blocks:
+            for conv, bn in ((blk.conv1, blk.bn1), (blk.conv2, blk.bn2)):
+                w, b = fold(conv, bn)
+                ws.append(_pack_conv(w))
+                bs.append(b)
+        wp, bp = fold(t.conv_policy, t.policy_bn)
+        wv, bv = fold(t.conv_value, t.value_bn)
+        ws.append(_pack_conv(torch.cat([wp, wv], 0)))
+        bs.append(torch.cat([bp, bv], 0))
+        self.n_blocks = len(t.residual_blocks)
+        self.wblob = torch.cat(ws).to(dev).contiguous()
+        self.bblob = torch.cat([x.float() for x in bs]).to(dev).contiguous()
+        ff, cells = t.filter_factor, self.W * self.H
+
+        def nhwc_cols(lin):
+            m = lin.weight.detach()
+            return m.view(m.shape[0], ff, self.W, self.H).permute(0, 2, 3, 1).reshape(m.shape[0], -1)
+
+        bf = torch.bfloat16
+        self.lp_w = nhwc_cols(t.linear_policy).to(dev, bf).contiguous()
+        self.lp_b = t.linear_policy.bias.detach().to(dev, bf)
+        self.fv_w = nhwc_cols(t.fc_value).to(dev, bf).contiguous()
+        self.fv_b = t.fc_value.bias.detach().to(dev, bf)
+        self.lo_w = t.linear_output.weight.detach().to(dev, bf)
+        self.lo_b = t.linear_output.bias.detach().to(dev, bf)
+        self.ff, self.cells = ff, cells
+        t.train(was)
+
+    @torch.no_grad()
+    def trunk(self, planes_nhwc):
+        """planes: bf16 [n, W, H, 3] contiguous -> head features bf16 [n, cells, C/2]."""
+        n = planes_nhwc.shape[0]
+        feats = torch.empty((max(n, 1), self.cells, self.C // 2), dtype=torch.bfloat16, device=planes_nhwc.device)
+        if n:
+            stream = torch.cuda.current_stream().cuda_stream
+            rc = self._lib.lib().spmcts_tower_forward(
+                self.W, self.H, self.C, self.n_blocks, self._lib.ctypes.c_void_p(planes_nhwc.data_ptr()), n,
+                self._lib.ctypes.c_void_p(self.wblob.data_ptr()), self._lib.ctypes.c_void_p(self.bblob.data_ptr()),
+                self._lib.ctypes.c_void_p(feats.data_ptr()), self._lib.ctypes.c_void_p(stream))
+            if rc != 0:
+                raise self._lib.SpmctsError(f"spmcts_tower_forward failed ({rc})")
+        return feats[:n]
+
+    @torch.no_grad()
+    def __call__(self, leaves):
+        # leaves: NCHW view over NHWC storage (arena leaf buffer) or any [n, 3, W, H] planes
+        planes = leaves.permute(0, 2, 3, 1)
+        if planes.dtype != torch.bfloat16 or not planes.is_contiguous():
+            planes = planes.to(torch.bfloat16).contiguous()
+        n = planes.shape[0]
+        f = self.trunk(planes)
+        pf = f[:, :, : self.ff].reshape(n, -1)
+        vf = f[:, :, self.ff:].reshape(n, -1)
+        probs = torch.softmax(torch.nn.functional.linear(pf, self.lp_w, self.lp_b).float(), dim=1)
+        v = torch.relu(torch.nn.functional.linear(vf, self.fv_w, self.fv_b))
+        value = torch.tanh(torch.nn.functional.linear(v, self.lo_w, self.lo_b).float()).reshape(-1)
+        return probs.contiguous(), value.contiguous()

@@ -1,0 +1,320 @@
+"""`SelfPlayScheduler` with the reference API, driving the device arena.
+
+Drop-in for games/algos/self_play_parallel.py:44-379.  The constructor takes
+the same arguments (plus the stale `self_play=` its own callers pass,
+run_self_play_connect4.py:61, elo.py:81), and `train_model`,
+`compare_models`, `evaluate_policy`, `run_evaluation_games`,
+`parse_results`, `setup_player_workers`, `setup_update_worker` keep their
+signatures.  What changes is underneath:
+
+  * instead of (cpu_count - 2) SelfPlayWorker processes x threads_per_worker
+    games x thread_count search threads + an InferenceWorker over
+    multiprocessing queues, ONE SelfPlayEngine per GPU runs `n_games`
+    concurrent games in lock step (all leaves of all games = one network
+    batch);
+  * the memory queue, result queue and task queue are in-process objects with
+    the same put/get/empty surface (results carry the reference's
+    {"reward", "swap_sides"} dicts, moves are `Move` namedtuples);
+  * the UpdateWorker's training (updateworker.py:141-149: AlphaZero loss, SGD
+    lr/momentum 0.9/wd 1e-4, 100 steps per update call, checkpoint
+    {"model": state_dict} per epoch, LR on plateau) runs in-process between
+    plies on the same GPU; self-play uses the epoch-start weights, refreshed at
+    each epoch boundary exactly like the reference's epoch_value reload.
+
+With torchrun and WORLD_SIZE > 1, every rank plays its own shard of games;
+Move records and episode statistics are gathered to rank 0 (distributed.py).
+"""
+import datetime
+import logging
+import os
+import time
+from collections import deque
+
+import numpy as np
+import torch
+
+from . import distributed as D
+from .arena import GAMES, game_of_env
+from .engine import SelfPlayEngine
+from .mcts import MCTreeSearch, Move
+
+
+class LocalQueue:
+    """In-process stand-in for the multiprocessing queues (put / get / empty / qsize)."""
+
+    def __init__(self):
+        self._q = deque()
+
+    def put(self, item):
+        self._q.append(item)
+
+    def get(self, block=True, timeout=None):
+        return self._q.popleft()
+
+    def empty(self):
+        return not self._q
+
+    def qsize(self):
+        return len(self._q)
+
+    def join(self):
+        pass
+
+    def task_done(self):
+        pass
+
+
+def moves_to_records(moves, W, H):
+    """Arena export rows -> Move namedtuples (mcts.py:17; dtypes as mcts.py:282-288, :230)."""
+    st = moves["state"].cpu().numpy().astype(np.int64)
+    tp = moves["tree_probs"].cpu()
+    q = moves["q"].cpu().numpy()
+    qf = moves["q_f64"].cpu().numpy()
+    z = moves["z"].cpu()
+    out = []
+    for i in range(len(z)):
+        qt = torch.tensor(float(q[i]), dtype=torch.float64 if qf[i] else torch.float32)
+        out.append(Move(torch.as_tensor(st[i].reshape(W, H)), z[i].clone(), tp[i].clone(), qt))
+    return out
+
+
+class SelfPlayScheduler:
+    def __init__(self, policy_container, env, evaluation_policy_container=None, network=None, swap_sides=True,
+                 save_dir="saves", epoch_length=500, initial_games=64, lr=0.001, stagger=False, evaluation_games=100,
+                 evaluation_network=None, stagger_mem_step=5000, deduplicate=False, update_delay=0.01,
+                 self_play=None, n_games=None, device=None, seed=0, updates_per_ply=4):
+        self.policy_container = policy_container
+        self.evaluation_policy_container = evaluation_policy_container
+        self.env_gen = env
+        self.game = game_of_env(env)
+        _, self.W, self.H, self.A = GAMES[self.game]
+        self.swap_sides = swap_sides
+        self.save_dir = save_dir
+        self.epoch_length = epoch_length
+        self.initial_games = initial_games
+        self.lr = lr
+        self.stagger = stagger
+        self.stagger_mem_step = stagger_mem_step
+        self.deduplicate = deduplicate
+        self.update_delay = update_delay
+        self.evaluation_games = evaluation_games
+        self.evaluation_network = evaluation_network
+        self.network = self._get_network(network, policy_container)
+        self.seed = seed
+        self.updates_per_ply = updates_per_ply
+        rank, world, local = D.env_rank()
+        self.rank, self.world = rank, world
+        self.device = torch.device(device) if device is not None else torch.device(
+            "cuda", local if torch.cuda.is_available() else 0)
+        self.n_games = n_games
+        self.start_time = datetime.datetime.now().isoformat()
+        self.task_queue = LocalQueue()
+        self.memory_queue = LocalQueue()
+        self.result_queue = LocalQueue()
+        self.engine = None
+        self.trainer = None
+        self.epoch_value = 0
+        if save_dir and rank == 0:
+            os.makedirs(os.path.join(save_dir, self.start_time), exist_ok=True)
+
+    # ------------------------------------------------------------------ reference helpers
+    def _get_network(self, network, container):
+        """self_play_parallel.py:173-184"""
+        if network is not None:
+            return network
+        if container is None:
+            return None
+        if container.policy_kwargs.get("network") is not None:
+            return container.policy_kwargs.pop("network")
+        if container.policy_kwargs.get("evaluator") is not None:  # deprecated key
+            return container.policy_kwargs.pop("evaluator")
+        return None
+
+    def _policy_kwargs(self):
+        kw = dict(self.policy_container.policy_kwargs)
+        return kw
+
+    def setup_player_workers(self, num_workers=None, inference_proxy=True, threads_per_worker=8, resume_model=False):
+        """Build the device self-play engine (replaces the worker processes, :95-171)."""
+        kw = self._policy_kwargs()
+        n_games = self.n_games or max(64, min(4096, (num_workers or 1) * threads_per_worker * 64))
+        if resume_model:
+            self._load_latest(prev_run=True)
+        self.engine = SelfPlayEngine(self.game, self.network, n_games=n_games,
+                                     iterations=kw.get("iterations", 100), alpha=kw.get("alpha", 1),
+                                     strong_play=kw.get("strong_play", False), seed=self.seed + 7919 * self.rank,
+                                     device=self.device)
+        return self.engine, None, self.epoch_value
+
+    def setup_update_worker(self, resume_memory=False, resume_model=False):
+        """The trainer (updateworker.py:16-149) as an in-process MCTreeSearch-style policy."""
+        kw = self._policy_kwargs()
+        self.network.to(self.device)
+        optim = torch.optim.SGD(self.network.parameters(), weight_decay=0.0001, momentum=0.9, lr=self.lr)
+        self.trainer = _Trainer(self.network, optim, memory_size=kw.get("memory_size", 200000),
+                                batch_size=kw.get("batch_size", 64), min_memory=kw.get("min_memory", 20000),
+                                q_average=kw.get("q_average", True), device=self.device)
+        if resume_model:
+            self._load_latest(prev_run=True)
+        return self.trainer, None, None
+
+    def _load_latest(self, prev_run=False):
+        from glob import glob
+
+        runs = sorted(d for d in glob(os.path.join(self.save_dir, "*")) if os.path.isdir(d)
+                      and (not prev_run or os.path.basename(d) != self.start_time) and os.listdir(d))
+        if not runs:
+            return None
+        saves = sorted(glob(os.path.join(runs[-1], "model*")))
+        if not saves:
+            return None
+        ck = torch.load(saves[-1], weights_only=True, map_location="cpu")
+        self.network.load_state_dict(ck["model"])
+        return saves[-1]
+
+    # ------------------------------------------------------------------ self-play
+    def _play_games(self, n_games, update=True):
+        """Play `n_games` self-play games over all ranks; Moves -> memory_queue, results -> result_queue."""
+        eng = self.engine
+        per_rank = n_games // self.world + (1 if self.rank < n_games % self.world else 0)
+        eng.max_games = eng.games_done + per_rank
+        eng.arena.games_set_limit(eng.arena.counters()["games_finished"] + per_rank)
+        if not eng.started:
+            eng.start()
+        else:
+            # restart empty slots up to the new budget
+            st = eng.arena.games_state()
+            idle = [i for i, s in enumerate(st["state"]) if s == 0][:per_rank]
+            if idle:
+                eng.arena.games_start(idle)
+
+        def on_moves(m):
+            g = D.gather_moves(m, self.W * self.H, self.A) if D.is_distributed() else m
+            if g is None:
+                return
+            for rec in moves_to_records(g, self.W, self.H):
+                if update:
+                    self.memory_queue.put(rec)
+            z_first = {}
+            for gid, z in zip(g["game"].cpu().tolist(), g["z"].cpu().tolist()):
+                z_first.setdefault(gid, z)
+            for gid, z in z_first.items():
+                self.result_queue.put({"reward": int(z), "swap_sides": bool(gid % 2)})
+
+        while eng.games_done < eng.max_games:
+            eng.ply(on_moves=on_moves)
+            if update and self.trainer is not None:
+                self.trainer.pull(self.memory_queue)
+                for _ in range(self.updates_per_ply):
+                    self.trainer.step()
+        eng.check()
+
+    def train_model(self, num_epochs=10, resume_model=False, resume_memory=False, num_workers=None,
+                    threads_per_worker=8, inference_proxy=True):
+        """self_play_parallel.py:213-291"""
+        self.setup_player_workers(num_workers=num_workers, threads_per_worker=threads_per_worker,
+                                  resume_model=resume_model, inference_proxy=inference_proxy)
+        self.setup_update_worker(resume_memory=resume_memory, resume_model=resume_model)
+        logging.info(f"generating {self.initial_games} initial games")
+        self._play_games(self.initial_games, update=True)
+        while not self.result_queue.empty():
+            self.result_queue.get()
+        if self.evaluation_games:
+            self.evaluate_policy(-1)
+        for epoch in range(num_epochs):
+            self._play_games(self.epoch_length, update=True)
+            saved = os.path.join(self.save_dir, self.start_time,
+                                 "model-" + datetime.datetime.now().isoformat() + ":" + str(self.epoch_length * (epoch + 1)))
+            if self.rank == 0:
+                torch.save({"model": self.network.state_dict()}, saved)
+            D.broadcast_state_dict(self.network)
+            self.engine.refresh_network()  # epoch_value reload (selfplayworker.py:109-114)
+            self.epoch_value += 1
+            if self.stagger:
+                m = self.trainer.memory
+                m.change_size(min(m.max_size + self.stagger_mem_step, 1500000))
+            reward = self.evaluate_policy(epoch)
+            self.trainer.lr_step(reward)
+
+    def run_evaluation_games(self):
+        """self_play_parallel.py:294-300 — needs a two-network arena."""
+        if self.evaluation_policy_container is None:
+            return
+        logging.info("evaluation games against a separate policy are not implemented on the arena yet")
+
+    def parse_results(self, reward_list):
+        """self_play_parallel.py:302-327"""
+        if not reward_list:
+            return 0, {"first": dict(wins=0, draws=0, losses=0), "second": dict(wins=0, draws=0, losses=0)}
+        win_percent = sum(1 if r["reward"] > 0 else 0 for r in reward_list) / len(reward_list) * 100
+        wins = len([i for i in reward_list if i["reward"] == 1])
+        draws = len([i for i in reward_list if i["reward"] == 0])
+        losses = len([i for i in reward_list if i["reward"] == -1])
+        print(f"win percent : {win_percent}%")
+        print(f"wins: {wins}, draws: {draws}, losses: {losses}")
+        breakdown = {}
+        for j, start in enumerate(["first", "second"]):
+            sel = [i for i in reward_list if i["swap_sides"] == bool(j)]
+            breakdown[start] = dict(wins=len([i for i in sel if i["reward"] == 1]),
+                                    draws=len([i for i in sel if i["reward"] == 0]),
+                                    losses=len([i for i in sel if i["reward"] == -1]))
+        total_rewards = int(np.sum([r["reward"] for r in reward_list]))
+        return total_rewards, breakdown
+
+    def evaluate_policy(self, epoch):
+        reward_list = []
+        while not self.result_queue.empty():
+            reward_list.append(self.result_queue.get())
+        total = 0
+        if epoch >= 0 and reward_list:
+            total, _ = self.parse_results(reward_list)
+        self.run_evaluation_games()
+        return total
+
+    def compare_models(self, num_workers=None, inference_proxy=True, threads_per_worker=8, resume_model=False):
+        """self_play_parallel.py:355-379 with both sides MCTreeSearch on the arena (policy vs evaluation net)."""
+        raise NotImplementedError("two-network arena evaluation is the next milestone (SURVEY §8(f) rank 3)")
+
+
+class _Trainer:
+    """UpdateWorker core (updateworker.py:119-149) on the same device: pull, AZ-loss SGD steps, LR on plateau."""
+
+    def __init__(self, network, optim, memory_size, batch_size, min_memory, q_average, device):
+        from .memory import Memory
+
+        self.network = network
+        self.optim = optim
+        self.memory = Memory(memory_size)
+        self.batch_size = batch_size
+        self.min_memory = min_memory
+        self.q_average = q_average
+        self.device = device
+        self.scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optim, "max", patience=15, factor=0.5,
+                                                                    min_lr=0.00001, cooldown=5)
+
+    def pull(self, queue):
+        while not queue.empty():
+            self.memory.add(queue.get())
+
+    def step(self):
+        if len(self.memory) < max(self.batch_size, self.min_memory):
+            return None
+        self.network.train()
+        batch = self.memory.sample(self.batch_size)
+        s, z, pi, q = Move(*zip(*batch))
+        probs, value = self.network.forward(torch.stack(s).to(self.device))
+        z = torch.stack(z).to(self.device).float()
+        if self.q_average:
+            z = z + torch.stack(q).to(self.device).float()
+        value_loss = torch.mean((value.view(-1) - z) ** 2)
+        pi = torch.stack(pi).to(self.device).float()
+        prob_loss = -(probs.log() * pi).sum() / probs.size(0)
+        loss = value_loss + prob_loss
+        self.optim.zero_grad()
+        loss.backward()
+        self.optim.step()
+        self.network.eval()
+        return float(loss)
+
+    def lr_step(self, reward):
+        self.scheduler.step(reward)
