@@ -102,10 +102,12 @@ class SelfPlayEngine:
         self.nn_timer = EventTimer() if on else None
 
     def start(self):
+        """Fill every slot and keep refilling (until `max_games` games have started, if set)."""
         a = self.arena
         first = self.n_games if self.max_games is None else min(self.n_games, self.max_games)
         a.games_set_limit(-1 if self.max_games is None else self.max_games)
         a.games_start(list(range(first)))
+        self._started = first if self.max_games is None else self.max_games
         self.started = True
 
     def _eval_expand(self, n):
@@ -159,6 +161,33 @@ class SelfPlayEngine:
             if self.max_games is not None and self.games_done >= self.max_games:
                 break
         return dict(plies=n, seconds=time.time() - t0, games=self.games_done, positions=self.positions)
+
+    def play_games(self, n, on_moves=None, on_ply=None):
+        """Play exactly `n` more games (refilling slots on device until n have started).
+
+        Returns the number of plies it took.  Game ids continue from earlier calls, so
+        swap_sides alternates across calls exactly as the reference's task ids do."""
+        a = self.arena
+        if n <= 0:
+            return 0
+        started = getattr(self, "_started", 0)
+        limit = started + n
+        a.games_set_limit(limit)
+        st = a.games_state()
+        idle = [i for i, s in enumerate(st["state"]) if s == 0]
+        k = min(len(idle), n)
+        if k:
+            a.games_start(idle[:k])
+        self.started = True
+        target = self.games_done + n
+        plies = 0
+        while self.games_done < target:
+            self.ply(on_moves=on_moves)
+            plies += 1
+            if on_ply is not None:
+                on_ply(self)
+        self._started = limit
+        return plies
 
     def counters(self):
         return self.arena.counters()

@@ -174,39 +174,32 @@ class SelfPlayScheduler:
 
     # ------------------------------------------------------------------ self-play
     def _play_games(self, n_games, update=True):
-        """Play `n_games` self-play games over all ranks; Moves -> memory_queue, results -> result_queue."""
+        """Play `n_games` self-play games over all ranks (task ids i -> swap_sides = i odd,
+        self_play_parallel.py:236-238); Moves -> memory_queue (rank 0), results -> result_queue."""
         eng = self.engine
         per_rank = n_games // self.world + (1 if self.rank < n_games % self.world else 0)
-        eng.max_games = eng.games_done + per_rank
-        eng.arena.games_set_limit(eng.arena.counters()["games_finished"] + per_rank)
-        if not eng.started:
-            eng.start()
-        else:
-            # restart empty slots up to the new budget
-            st = eng.arena.games_state()
-            idle = [i for i, s in enumerate(st["state"]) if s == 0][:per_rank]
-            if idle:
-                eng.arena.games_start(idle)
 
         def on_moves(m):
             g = D.gather_moves(m, self.W * self.H, self.A) if D.is_distributed() else m
             if g is None:
                 return
-            for rec in moves_to_records(g, self.W, self.H):
-                if update:
+            if update:
+                for rec in moves_to_records(g, self.W, self.H):
                     self.memory_queue.put(rec)
-            z_first = {}
+            first = {}
             for gid, z in zip(g["game"].cpu().tolist(), g["z"].cpu().tolist()):
-                z_first.setdefault(gid, z)
-            for gid, z in z_first.items():
+                first.setdefault(gid, z)  # the policy's Moves come first: z = r (policy's view)
+            for gid, z in first.items():
                 self.result_queue.put({"reward": int(z), "swap_sides": bool(gid % 2)})
 
-        while eng.games_done < eng.max_games:
-            eng.ply(on_moves=on_moves)
+        def on_ply(_):
+            D.all_reduce_stats(eng.stats_vector())
             if update and self.trainer is not None:
                 self.trainer.pull(self.memory_queue)
                 for _ in range(self.updates_per_ply):
                     self.trainer.step()
+
+        eng.play_games(per_rank, on_moves=on_moves, on_ply=on_ply)
         eng.check()
 
     def train_model(self, num_epochs=10, resume_model=False, resume_memory=False, num_workers=None,

@@ -1,0 +1,74 @@
+"""CPU: the multi-GPU exchange steps (episode-stat all_reduce, Move gather to rank 0,
+weight broadcast) with torch.distributed gloo, world size 2."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from self_play_reinforcement_learning_amd import distributed as D
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _moves(rank, n):
+    g = torch.Generator().manual_seed(rank)
+    return dict(
+        state=torch.randint(-1, 2, (n, 42), dtype=torch.int8, generator=g),
+        tree_probs=torch.rand(n, 7, generator=g),
+        q=torch.rand(n, generator=g, dtype=torch.float64),
+        q_f64=torch.randint(0, 2, (n,), dtype=torch.uint8, generator=g),
+        z=torch.randint(-1, 2, (n,), generator=g).float(),
+        game=torch.arange(n, dtype=torch.int64) + 1000 * rank,
+    )
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    D.init_from_env(backend="gloo")
+    stats = D.all_reduce_stats([rank + 1, 10 * rank, 1, 0, 0, 0, 1, 0])
+    got = D.gather_moves(_moves(rank, 3 + 2 * rank), 42, 7)
+    mx = D.all_reduce_max(float(rank) * 1.5)
+    net = torch.nn.Linear(4, 2)
+    with torch.no_grad():
+        net.weight.fill_(float(rank))
+    D.broadcast_state_dict(net)
+    q.put((rank, stats.tolist(), None if got is None else {k: v.clone() for k, v in got.items()}, mx,
+           float(net.weight.sum())))
+    torch.distributed.destroy_process_group()
+
+
+def test_pack_unpack_roundtrip():
+    m = _moves(0, 9)
+    back = D.unpack_moves(D.pack_moves(m), 42, 7)
+    for k in m:
+        assert torch.equal(back[k].reshape(m[k].shape), m[k]), k
+
+
+def test_two_rank_exchange_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in procs], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, s0, g0, mx0, w0), (r1, s1, g1, mx1, w1) = res
+    assert s0 == s1 == [3, 10, 2, 0, 0, 0, 2, 0]
+    assert mx0 == mx1 == 1.5
+    assert w0 == w1 == 0.0  # rank 0's weights everywhere
+    assert g1 is None
+    exp = {k: torch.cat([_moves(0, 3)[k], _moves(1, 5)[k]]) for k in g0}
+    for k in exp:
+        assert torch.equal(g0[k].reshape(exp[k].shape), exp[k]), k
