@@ -42,7 +42,7 @@ struct Cfg {
   static constexpr int NT = ROWS / 32;  // 32-cell tiles
   static constexpr int MT = C / 128;    // 32-channel tiles per wave (4 waves)
   static constexpr int BUF = (ROWS + 1) * RS;
-  static constexpr int LDS = 2 * BUF + 9 * ROWS * 2;
+  static constexpr int LDS = 2 * BUF;
   static constexpr int HEAD = C / 2;  // policy filter_factor | value filter_factor channels (filter_factor = C/4)
   static constexpr int HCT = HEAD / 32;  // head channel tiles
   static_assert(MT * NT == 8, "tile plan assumes 8 accumulator tiles per wave");
@@ -53,10 +53,45 @@ struct Cfg {
 __device__ __forceinline__ bf16x8 lds_b128(const char *p) { return *(const bf16x8 *)p; }
 
 // One conv layer over the resident tile: src (LDS) -> dst (LDS), optional residual (LDS, == dst).
-// KK = input channels / 16 (k-steps per tap), TAPS = 9 (3x3) or 1 (1x1, centre only).
+// KK = input channels / 16 (k-steps per tap), TAPS = 9 (3x3).
+// Software pipeline: the 8 B (activation) fragments of step s+1 are read from LDS while
+// the MFMAs of step s run, and the A (weight) fragment is fetched DEPTH steps ahead from
+// L2/MALL (~4 x 256 MFMA cycles of cover for the memory latency).
+// Per-lane neighbour geometry: for each of the wave's cell tiles t, the byte offset of the
+// lane's cell row and a 9-bit mask of the taps whose neighbour lies on the board.
+template <class K>
+struct Nbr {
+  int base[K::NT];
+  uint32_t mask[K::NT];
+  __device__ __forceinline__ void init(int r) {
+#pragma unroll
+    for (int t = 0; t < K::NT; ++t) {
+      const int row = t * 32 + r;
+      base[t] = row * K::RS;
+      uint32_t m = 0;
+      if (row < K::VROWS) {
+        const int c = row % K::CELLS, x = c / K::H, y = c % K::H;
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+          const int nx = x + tap / 3 - 1, ny = y + tap % 3 - 1;
+          if (nx >= 0 && nx < K::W && ny >= 0 && ny < K::H) m |= 1u << tap;
+        }
+      }
+      mask[t] = m;
+    }
+  }
+  // byte offset of the source row of tile t for `tap` (the zero row when off the board)
+  __device__ __forceinline__ int off(int t, int tap) const {
+    const int d = ((tap / 3 - 1) * K::H + (tap % 3 - 1)) * K::RS;
+    return ((mask[t] >> tap) & 1u) ? base[t] + d : K::ZROW * K::RS;
+  }
+};
+
 template <class K, int KK, int TAPS, bool RESID>
-__device__ __forceinline__ void conv_layer(const char *src, char *dst, const int16_t *tapt, const bf16x8 *w,
+__device__ __forceinline__ void conv_layer(const char *src, char *dst, const Nbr<K> &nb, const bf16x8 *w,
                                            const float *bias, int wave, int lane) {
+  constexpr int STEPS = TAPS * KK;
+  constexpr int DEPTH = (KK % 4 == 0) ? 4 : 1;
   const int r = lane & 31, h = lane >> 5;
   f32x16 acc[K::MT][K::NT];
 #pragma unroll
@@ -66,35 +101,62 @@ __device__ __forceinline__ void conv_layer(const char *src, char *dst, const int
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[m][t][i] = 0.f;
 
-  // weight fragment index of (ctile, tap, kk): ((ct * TAPS + tap) * KK + kk) * 64 + lane
-  constexpr int STEPS = TAPS * KK;
-  bf16x8 a_cur[K::MT], a_nxt[K::MT];
+  // weight fragment of (ctile, step s): w[(ct * STEPS + s) * 64 + lane]
+  const bf16x8 *wl[K::MT];
 #pragma unroll
-  for (int m = 0; m < K::MT; ++m) a_cur[m] = w[((size_t)(wave * K::MT + m) * STEPS) * 64 + lane];
+  for (int m = 0; m < K::MT; ++m) wl[m] = w + (size_t)(wave * K::MT + m) * STEPS * 64 + lane;
+  bf16x8 a[DEPTH][K::MT];
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d)
+#pragma unroll
+    for (int m = 0; m < K::MT; ++m) a[d][m] = wl[m][(size_t)d * 64];
+
+  const int hoff = 16 * h;  // byte offset of this lane's 8 channels inside a 16-channel k-step
+  int off_cur[K::NT], off_nxt[K::NT];
+#pragma unroll
+  for (int t = 0; t < K::NT; ++t) off_cur[t] = nb.off(t, 0) + hoff;
+  bf16x8 bc[K::NT], bn[K::NT];
+#pragma unroll
+  for (int t = 0; t < K::NT; ++t) bc[t] = lds_b128(src + off_cur[t]);
 
   for (int tap = 0; tap < TAPS; ++tap) {
-    int rows[K::NT];
-    const int tap_id = TAPS == 1 ? 4 : tap;
+    if (tap + 1 < TAPS) {
 #pragma unroll
-    for (int t = 0; t < K::NT; ++t) rows[t] = tapt[tap_id * K::ROWS + t * 32 + r];
+      for (int t = 0; t < K::NT; ++t) off_nxt[t] = nb.off(t, tap + 1) + hoff;
+    }
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
       const int s = tap * KK + kk;
-      if (s + 1 < STEPS) {
+      // B fragments of step s + 1
+      if (kk + 1 < KK) {
+#pragma unroll
+        for (int t = 0; t < K::NT; ++t) bn[t] = lds_b128(src + off_cur[t] + (kk + 1) * 32);
+      } else if (tap + 1 < TAPS) {
+#pragma unroll
+        for (int t = 0; t < K::NT; ++t) bn[t] = lds_b128(src + off_nxt[t]);
+      }
+      const int slot = DEPTH == 1 ? 0 : (kk % DEPTH);
+      bf16x8 acur[K::MT];
+#pragma unroll
+      for (int m = 0; m < K::MT; ++m) acur[m] = a[slot][m];
+      // A fragment of step s + DEPTH
+      if (s + DEPTH < STEPS) {
+#pragma unroll
+        for (int m = 0; m < K::MT; ++m) a[slot][m] = wl[m][(size_t)(s + DEPTH) * 64];
+      }
+      // keep the prefetches ahead of this step's MFMAs (hipcc otherwise sinks them just-in-time)
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < K::NT; ++t)
 #pragma unroll
         for (int m = 0; m < K::MT; ++m)
-          a_nxt[m] = w[((size_t)(wave * K::MT + m) * STEPS + s + 1) * 64 + lane];
-      }
-      const int koff = (kk * 16 + 8 * h) * 2;
+          acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[m], bc[t], acc[m][t], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int t = 0; t < K::NT; ++t) {
-        const bf16x8 b = lds_b128(src + rows[t] * K::RS + koff);
-#pragma unroll
-        for (int m = 0; m < K::MT; ++m) acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_cur[m], b, acc[m][t], 0, 0, 0);
-      }
-#pragma unroll
-      for (int m = 0; m < K::MT; ++m) a_cur[m] = a_nxt[m];
+      for (int t = 0; t < K::NT; ++t) bc[t] = bn[t];
     }
+#pragma unroll
+    for (int t = 0; t < K::NT; ++t) off_cur[t] = off_nxt[t];
   }
   // epilogue: bias (+ residual) + ReLU -> bf16 rows of dst
 #pragma unroll
@@ -183,26 +245,16 @@ __device__ __forceinline__ void head_layer(const char *src, const bf16x8 *w, con
 // lane l of fragment (ct, tap, kk) holds W[ct*32 + (l & 31)][tap][kk*16 + 8*(l >> 5) + j], j = 0..7.
 // bias: stem C, blocks 2*C each, head C/2.
 template <class K>
-__global__ __launch_bounds__(256) void k_tower(const __bf16 *planes, int batch, int n_blocks, const bf16x8 *wpk,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_tower(const __bf16 *planes, int batch, int n_blocks, const bf16x8 *wpk,
                                                const float *bias, __bf16 *out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char *X = smem;
   char *Y = smem + K::BUF;
-  int16_t *tapt = (int16_t *)(smem + 2 * K::BUF);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int board0 = blockIdx.x * K::BOARDS;
+  Nbr<K> nb;
+  nb.init(lane & 31);
 
-  // neighbour table: tapt[tap][row] = source row of (row's cell shifted by tap) or ZROW
-  for (int i = tid; i < 9 * K::ROWS; i += 256) {
-    const int tap = i / K::ROWS, row = i % K::ROWS;
-    int src = K::ZROW;
-    if (row < K::VROWS) {
-      const int cell = row % K::CELLS, x = cell / K::H, y = cell % K::H;
-      const int nx = x + tap / 3 - 1, ny = y + tap % 3 - 1;
-      if (nx >= 0 && nx < K::W && ny >= 0 && ny < K::H) src = row - cell + nx * K::H + ny;
-    }
-    tapt[i] = (int16_t)src;
-  }
   // zero rows + stem input: Y rows hold 16 channels (3 planes, 13 zeros)
   for (int i = tid; i < K::RS / 4; i += 256) {
     ((uint32_t *)(X + K::ZROW * K::RS))[i] = 0u;
@@ -220,16 +272,16 @@ __global__ __launch_bounds__(256) void k_tower(const __bf16 *planes, int batch, 
 
   const bf16x8 *w = wpk;
   const float *b = bias;
-  conv_layer<K, 1, 9, false>(Y, X, tapt, w, b, wave, lane);
+  conv_layer<K, 1, 9, false>(Y, X, nb, w, b, wave, lane);
   w += (size_t)K::C / 32 * 9 * 1 * 64;
   b += K::C;
   __syncthreads();
   for (int blk = 0; blk < n_blocks; ++blk) {
-    conv_layer<K, K::C / 16, 9, false>(X, Y, tapt, w, b, wave, lane);
+    conv_layer<K, K::C / 16, 9, false>(X, Y, nb, w, b, wave, lane);
     w += (size_t)K::C / 32 * 9 * (K::C / 16) * 64;
     b += K::C;
     __syncthreads();
-    conv_layer<K, K::C / 16, 9, true>(Y, X, tapt, w, b, wave, lane);
+    conv_layer<K, K::C / 16, 9, true>(Y, X, nb, w, b, wave, lane);
     w += (size_t)K::C / 32 * 9 * (K::C / 16) * 64;
     b += K::C;
     __syncthreads();
