@@ -217,6 +217,17 @@ int spmcts_table_net(int32_t game, int32_t width, int32_t height, const void *le
 int spmcts_tower_forward(int32_t width, int32_t height, int32_t channels, int32_t n_blocks, const void *planes_dev,
                          int32_t batch, const void *weights_dev, const float *bias_dev, void *features_dev,
                          spmcts_stream stream);
+/* The linear heads on the trunk features (modules.py:96-105), fused: policy softmax over
+ * `actions` and tanh value.  head_w: bf16 [32 (policy, zero-padded)][K] ++ [8ff][K],
+ * K = W*H*ff, columns in (cell, channel) order; head_b: f32 bp[32] ++ bv[8ff] ++ wo[8ff] ++ bo. */
+int spmcts_tower_heads(int32_t width, int32_t height, int32_t channels, int32_t actions, const void *features_dev,
+                       int32_t batch, const void *head_w_dev, const float *head_b_dev, float *probs_dev,
+                       float *values_dev, spmcts_stream stream);
+/* Head epilogue after one GEMM Z = features @ Wc^T (Wc rows: value hidden [hidden] then
+ * policy [actions]): value = tanh(relu(Z[:hidden] + bv) . wo + bo), probs = softmax(Z[hidden:] + bp).
+ * z_dev bf16 [batch][ldz]; head_b: f32 bv[hidden] ++ wo[hidden] ++ bo ++ bp[actions]. */
+int spmcts_head_epilogue(int32_t hidden, int32_t actions, const void *z_dev, int32_t ldz, int32_t batch,
+                         const float *head_b_dev, float *probs_dev, float *values_dev, spmcts_stream stream);
 int spmcts_tower_supported(int32_t width, int32_t height, int32_t channels);
 /* Memory-roofline helper: device copy bandwidth probe (bytes each way). */
 int spmcts_copy_probe(const void *src_dev, void *dst_dev, uint64_t bytes, spmcts_stream stream);

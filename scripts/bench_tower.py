@@ -23,7 +23,9 @@ b = torch.randint(-1, 2, (args.batch, 7, 6))
 x = planes_from_boards(b, 7, 6).cuda().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
 fl = resnet_flops_per_leaf(7, 6, 7, args.ff, args.blocks) * args.batch
 out = {}
-for name, ev in (("hip", HipTowerEvaluator(net)), ("torch_bf16", TowerEvaluator(net, dtype=torch.bfloat16))):
+for name, ev in (("hip", HipTowerEvaluator(net)), ("hip_fusedheads", HipTowerEvaluator(net, fused_heads=True)),
+                 ("hip_torchheads", HipTowerEvaluator(net, fused_heads=False)),
+                 ("torch_bf16", TowerEvaluator(net, dtype=torch.bfloat16))):
     for _ in range(3):
         ev(x)
     torch.cuda.synchronize()

@@ -113,6 +113,8 @@ _SIGS = {
     "spmcts_copy_probe": [_P, _P, _U64, _P],
     "spmcts_tower_forward": [_I32, _I32, _I32, _I32, _P, _I32, _P, _P, _P, _P],
     "spmcts_tower_supported": [_I32, _I32, _I32],
+    "spmcts_tower_heads": [_I32, _I32, _I32, _I32, _P, _I32, _P, _P, _P, _P, _P],
+    "spmcts_head_epilogue": [_I32, _I32, _P, _I32, _I32, _P, _P, _P, _P],
 }
 
 # every symbol the header declares (tests check the .so exports exactly these)

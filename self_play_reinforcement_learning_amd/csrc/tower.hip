@@ -289,6 +289,133 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   head_layer<K>(X, w, b, out, board0, batch, wave, lane);
 }
 
+// ---------------------------------------------------------------------------------------
+// Linear heads (modules.py:96-105 after the 1x1 convs), fused: for 32 boards per workgroup
+//   policy = softmax(pf @ Wp^T + bp)          pf = features[:, :, :ff]  (cell-major, K = cells*ff)
+//   value  = tanh(relu(vf @ Wv^T + bv) @ wo + bo)                     vf = features[:, :, ff:]
+// on v_mfma_f32_32x32x16_bf16 with M = 32 boards.  Weight blob (bf16): Wp padded to 32 rows
+// [32][K] then Wv [8ff][K]; float blob: bp[32] (padded), bv[8ff], wo[8ff], bo.
+template <int FF, int CELLS, int A>
+__global__ __launch_bounds__(256) void k_heads(const __bf16 *feats, int n, const __bf16 *hw, const float *hb,
+                                               float *probs, float *values) {
+  constexpr int K = CELLS * FF;
+  constexpr int KS = K / 16;
+  constexpr int HID = 8 * FF;
+  constexpr int VT = HID / 32;       // value hidden tiles
+  constexpr int VTW = VT / 4;        // per wave
+  static_assert(VT % 4 == 0 && FF % 16 == 0, "head tile plan");
+  __shared__ float s_part[4][32];  // per-wave value partial sums (fixed-order reduction: deterministic)
+  __shared__ float s_logit[32][33];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int b0 = blockIdx.x * 32;
+  const __bf16 *wp = hw;
+  const __bf16 *wv = hw + (size_t)32 * K;
+  const float *bp = hb, *bv = hb + 32, *wo = hb + 32 + HID, *bo = hb + 32 + 2 * HID;
+  const int board = b0 + r;
+  const bool ok = board < n;
+  const __bf16 *frow = feats + (size_t)(ok ? board : 0) * CELLS * 2 * FF;
+  f32x16 acc[VTW];
+  f32x16 pacc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) pacc[i] = 0.f;
+#pragma unroll
+  for (int v = 0; v < VTW; ++v)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[v][i] = 0.f;
+  const bf16x8 zero8 = {};
+  for (int s = 0; s < KS; ++s) {
+    const int k0 = 16 * s + 8 * h;
+    const int cell = k0 / FF, c = k0 % FF;
+    const bf16x8 av = ok ? *(const bf16x8 *)(frow + cell * 2 * FF + FF + c) : zero8;
+#pragma unroll
+    for (int v = 0; v < VTW; ++v) {
+      const int col = (wave * VTW + v) * 32 + r;
+      const bf16x8 bw = *(const bf16x8 *)(wv + (size_t)col * K + k0);
+      acc[v] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bw, acc[v], 0, 0, 0);
+    }
+    if (wave == 0) {
+      const bf16x8 ap = ok ? *(const bf16x8 *)(frow + cell * 2 * FF + c) : zero8;
+      const bf16x8 bw = *(const bf16x8 *)(wp + (size_t)r * K + k0);
+      pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap, bw, pacc, 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  // value: relu(acc + bv[col]) * wo[col], summed over the hidden units (cols)
+  // D layout: lane (r, h): col = r, rows (boards) = (i & 3) + 8 * (i >> 2) + 4 * h
+  float part[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) part[i] = 0.f;
+#pragma unroll
+  for (int v = 0; v < VTW; ++v) {
+    const int col = (wave * VTW + v) * 32 + r;
+    const float bb = bv[col], ww = wo[col];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) part[i] += fmaxf(acc[v][i] + bb, 0.f) * ww;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    float x = part[i];
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) x += __shfl_xor(x, off, 32);
+    part[i] = x;
+  }
+  if (r == 0) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s_part[wave][(i & 3) + 8 * (i >> 2) + 4 * h] = part[i];
+  }
+  if (wave == 0) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s_logit[(i & 3) + 8 * (i >> 2) + 4 * h][r] = pacc[i] + bp[r];
+  }
+  __syncthreads();
+  if (tid < 32) {
+    const int bd = b0 + tid;
+    if (bd < n) {
+      values[bd] = tanhf(((s_part[0][tid] + s_part[1][tid]) + (s_part[2][tid] + s_part[3][tid])) + bo[0]);
+      float m = -INFINITY;
+#pragma unroll
+      for (int a = 0; a < A; ++a) m = fmaxf(m, s_logit[tid][a]);
+      float e[A], sum = 0.f;
+#pragma unroll
+      for (int a = 0; a < A; ++a) {
+        e[a] = __expf(s_logit[tid][a] - m);
+        sum += e[a];
+      }
+      const float inv = 1.f / sum;
+#pragma unroll
+      for (int a = 0; a < A; ++a) probs[(size_t)bd * A + a] = e[a] * inv;
+    }
+  }
+}
+
+// Head epilogue after one GEMM  Z = features[n][cells*2ff] @ Wc^T  (Wc = value rows [8ff]
+// then policy rows [A], zero where a row meets the other head's channels):
+//   value = tanh(sum_j relu(Z[j] + bv[j]) * wo[j] + bo), probs = softmax(Z[8ff + a] + bp[a]).
+// One wave per board; the hidden-unit sum is a fixed-order lane reduction (deterministic).
+template <int HID, int A>
+__global__ __launch_bounds__(256) void k_head_epilogue(const __bf16 *Z, int ldz, int n, const float *hb,
+                                                       float *probs, float *values) {
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  if (wave >= n) return;
+  const __bf16 *z = Z + (size_t)wave * ldz;
+  const float *bv = hb, *wo = hb + HID, *bo = hb + 2 * HID, *bp = hb + 2 * HID + 1;
+  float acc = 0.f;
+#pragma unroll
+  for (int j = lane; j < HID; j += 64) acc += fmaxf((float)z[j] + bv[j], 0.f) * wo[j];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  float logit = lane < A ? (float)z[HID + lane] + bp[lane] : -INFINITY;
+  float m = logit;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+  const float e = lane < A ? __expf(logit - m) : 0.f;
+  float sum = e;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
+  if (lane < A) probs[(size_t)wave * A + lane] = e / sum;
+  if (lane == 0) values[wave] = tanhf(acc + bo[0]);
+}
+
 template <class K>
 static int launch(const void *planes, int batch, int n_blocks, const void *w, const float *b, void *out,
                   hipStream_t s) {
@@ -323,6 +450,54 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
   if (width == 3 && height == 3 && channels == 256)
     return launch<Cfg<256, 128, 3, 3>>(planes_dev, batch, n_blocks, weights_dev, bias_dev, features_dev, s);
   return -2;
+}
+
+extern "C" int spmcts_tower_heads(int32_t width, int32_t height, int32_t channels, int32_t actions,
+                                  const void *features_dev, int32_t batch, const void *head_w_dev,
+                                  const float *head_b_dev, float *probs_dev, float *values_dev, spmcts_stream stream) {
+  using namespace tower;
+  hipStream_t s = (hipStream_t)stream;
+  if (batch <= 0) return batch < 0 ? -3 : 0;
+  const int grid = (batch + 31) / 32;
+#define HEADS(FF, CELLS, A)                                                                                   \
+  hipLaunchKernelGGL((k_heads<FF, CELLS, A>), dim3(grid), dim3(256), 0, s, (const __bf16 *)features_dev, batch, \
+                     (const __bf16 *)head_w_dev, head_b_dev, probs_dev, values_dev)
+  if (width == 7 && height == 6 && actions == 7 && channels == 128)
+    HEADS(32, 42, 7);
+  else if (width == 7 && height == 6 && actions == 7 && channels == 256)
+    HEADS(64, 42, 7);
+  else if (width == 3 && height == 3 && actions == 9 && channels == 128)
+    HEADS(32, 9, 9);
+  else if (width == 3 && height == 3 && actions == 9 && channels == 256)
+    HEADS(64, 9, 9);
+  else
+    return -2;
+#undef HEADS
+  return hipGetLastError() == hipSuccess ? 0 : -11;
+}
+
+extern "C" int spmcts_head_epilogue(int32_t hidden, int32_t actions, const void *z_dev, int32_t ldz, int32_t batch,
+                                    const float *head_b_dev, float *probs_dev, float *values_dev,
+                                    spmcts_stream stream) {
+  using namespace tower;
+  hipStream_t s = (hipStream_t)stream;
+  if (batch <= 0) return batch < 0 ? -3 : 0;
+  const int grid = (batch + 3) / 4;
+#define EPI(HID, A)                                                                                       \
+  hipLaunchKernelGGL((k_head_epilogue<HID, A>), dim3(grid), dim3(256), 0, s, (const __bf16 *)z_dev, ldz, batch, \
+                     head_b_dev, probs_dev, values_dev)
+  if (hidden == 256 && actions == 7)
+    EPI(256, 7);
+  else if (hidden == 512 && actions == 7)
+    EPI(512, 7);
+  else if (hidden == 256 && actions == 9)
+    EPI(256, 9);
+  else if (hidden == 512 && actions == 9)
+    EPI(512, 9);
+  else
+    return -2;
+#undef EPI
+  return hipGetLastError() == hipSuccess ? 0 : -11;
 }
 
 extern "C" int spmcts_tower_supported(int32_t width, int32_t height, int32_t channels) {

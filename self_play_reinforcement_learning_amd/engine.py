@@ -73,7 +73,8 @@ class SelfPlayEngine:
                            device=self.device)
         self.n_games = n_games
         self.max_games = max_games
-        self.bucket = max(1, int(bucket))
+        # torch convolutions want few distinct shapes; the fused HIP tower takes any batch
+        self.bucket = max(1, int(getattr(self.evaluator, "bucket", bucket)))
         self.positions = 0
         self.games_done = 0
         self.nn_rows = 0

@@ -188,10 +188,14 @@ class HipTowerEvaluator(Evaluator):
 
     leaf_format = "bf16"
     leaf_layout = "nhwc"
+    bucket = 1  # the HIP kernels take any batch size; no shape padding needed
 
-    def __init__(self, tower, device=None):
+    def __init__(self, tower, device=None, fused_heads=True):
+        """fused_heads: True = MFMA heads kernel (deterministic, batch-independent), "gemm" =
+        one hipBLASLt GEMM + epilogue kernel, False = torch bf16 ops."""
         from . import _lib
 
+        self.fused_heads = fused_heads
         self._lib = _lib
         self.tower = tower
         self.device = device
@@ -245,6 +249,27 @@ class HipTowerEvaluator(Evaluator):
         self.lo_w = t.linear_output.weight.detach().to(dev, bf)
         self.lo_b = t.linear_output.bias.detach().to(dev, bf)
         self.ff, self.cells = ff, cells
+        # fused-heads blobs (csrc/tower.hip k_heads)
+        K = cells * ff
+        wp = torch.zeros(32, K, dtype=bf, device=dev)
+        wp[: self.A] = self.lp_w
+        self.head_w = torch.cat([wp.reshape(-1), self.fv_w.reshape(-1)]).contiguous()
+        bp = torch.zeros(32, dtype=torch.float32, device=dev)
+        bp[: self.A] = t.linear_policy.bias.detach().float().to(dev)
+        self.head_b = torch.cat([bp, t.fc_value.bias.detach().float().to(dev),
+                                 t.linear_output.weight.detach().float().reshape(-1).to(dev),
+                                 t.linear_output.bias.detach().float().reshape(-1).to(dev)]).contiguous()
+        # GEMM-heads blobs: Wc [hidden + A (padded to 16)][cells * 2ff] over the interleaved features
+        hid = 8 * ff
+        npad = -(-(hid + self.A) // 16) * 16
+        wc = torch.zeros(npad, cells, 2 * ff, dtype=torch.float32, device=dev)
+        wc[:hid, :, ff:] = nhwc_cols(t.fc_value).float().view(hid, cells, ff)
+        wc[hid:hid + self.A, :, :ff] = nhwc_cols(t.linear_policy).float().view(self.A, cells, ff)
+        self.wc = wc.reshape(npad, -1).to(bf).contiguous()
+        self.hid = hid
+        self.epi_b = torch.cat([t.fc_value.bias.detach().float(), t.linear_output.weight.detach().float().reshape(-1),
+                                t.linear_output.bias.detach().float().reshape(-1),
+                                t.linear_policy.bias.detach().float()]).to(dev).contiguous()
         t.train(was)
 
     @torch.no_grad()
@@ -270,6 +295,30 @@ class HipTowerEvaluator(Evaluator):
             planes = planes.to(torch.bfloat16).contiguous()
         n = planes.shape[0]
         f = self.trunk(planes)
+        if self.fused_heads == "gemm":
+            z = torch.matmul(f.reshape(n, -1), self.wc.t())  # one bf16 GEMM for both heads
+            probs = torch.empty((max(n, 1), self.A), dtype=torch.float32, device=f.device)
+            value = torch.empty(max(n, 1), dtype=torch.float32, device=f.device)
+            if n:
+                c = self._lib.ctypes.c_void_p
+                rc = self._lib.lib().spmcts_head_epilogue(
+                    self.hid, self.A, c(z.data_ptr()), z.shape[1], n, c(self.epi_b.data_ptr()), c(probs.data_ptr()),
+                    c(value.data_ptr()), c(torch.cuda.current_stream().cuda_stream))
+                if rc != 0:
+                    raise self._lib.SpmctsError(f"spmcts_head_epilogue failed ({rc})")
+            return probs[:n], value[:n]
+        if self.fused_heads:
+            probs = torch.empty((max(n, 1), self.A), dtype=torch.float32, device=f.device)
+            value = torch.empty(max(n, 1), dtype=torch.float32, device=f.device)
+            if n:
+                c = self._lib.ctypes.c_void_p
+                rc = self._lib.lib().spmcts_tower_heads(
+                    self.W, self.H, self.C, self.A, c(f.data_ptr()), n, c(self.head_w.data_ptr()),
+                    c(self.head_b.data_ptr()), c(probs.data_ptr()), c(value.data_ptr()),
+                    c(torch.cuda.current_stream().cuda_stream))
+                if rc != 0:
+                    raise self._lib.SpmctsError(f"spmcts_tower_heads failed ({rc})")
+            return probs[:n], value[:n]
         pf = f[:, :, : self.ff].reshape(n, -1)
         vf = f[:, :, self.ff:].reshape(n, -1)
         probs = torch.softmax(torch.nn.functional.linear(pf, self.lp_w, self.lp_b).float(), dim=1)

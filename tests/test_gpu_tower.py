@@ -49,6 +49,9 @@ def test_tower_matches_fp32_reference(game, blocks, ff):
     p, v = hip(xb)
     tb = TowerEvaluator(net, dtype=torch.bfloat16)
     p2, v2 = tb(xb)
+    for mode in (False, "gemm"):  # torch heads / GEMM + epilogue heads vs the default MFMA heads kernel
+        p3, v3 = HipTowerEvaluator(net, fused_heads=mode)(xb)
+        assert (p - p3).abs().max().item() < 1e-2 and (v - v3).abs().max().item() < 1e-2
     e_hip = max((p - ref_p).abs().max().item(), (v - ref_v.view(-1)).abs().max().item())
     e_bf = max((p2 - ref_p).abs().max().item(), (v2 - ref_v.view(-1)).abs().max().item())
     assert e_hip <= 2 * e_bf + 2e-3, (e_hip, e_bf)
