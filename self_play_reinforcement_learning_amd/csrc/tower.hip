@@ -21,6 +21,7 @@
 // + 42 x 64 head features, i.e. the activations never leave the CU.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "spmcts.h"
 
@@ -31,21 +32,24 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 
-template <int C_, int ROWS_, int W_, int H_>
+template <int C_, int ROWS_, int W_, int H_, int CG_ = 2>
 struct Cfg {
   static constexpr int C = C_, ROWS = ROWS_, W = W_, H = H_;
+  static constexpr int CG = CG_;        // waves split output channels into CG groups ...
+  static constexpr int MG = 4 / CG_;    // ... and cell rows into MG groups (4 waves)
   static constexpr int CELLS = W * H;
   static constexpr int BOARDS = ROWS / CELLS;
   static constexpr int VROWS = BOARDS * CELLS;
   static constexpr int RS = C * 2 + 16;  // bytes per LDS row
   static constexpr int ZROW = ROWS;
-  static constexpr int NT = ROWS / 32;  // 32-cell tiles
-  static constexpr int MT = C / 128;    // 32-channel tiles per wave (4 waves)
+  static constexpr int NT = ROWS / 32 / MG;  // 32-cell tiles per wave
+  static constexpr int MT = C / 32 / CG;     // 32-channel tiles per wave
   static constexpr int BUF = (ROWS + 1) * RS;
   static constexpr int LDS = 2 * BUF;
   static constexpr int HEAD = C / 2;  // policy filter_factor | value filter_factor channels (filter_factor = C/4)
   static constexpr int HCT = HEAD / 32;  // head channel tiles
-  static_assert(MT * NT == 8, "tile plan assumes 8 accumulator tiles per wave");
+  static_assert(MT >= 1 && NT >= 1 && MT * NT <= 8, "tile plan: at most 8 accumulator tiles per wave");
+  static_assert(CG * MG == 4, "4 waves");
   static_assert(BOARDS >= 1, "board larger than a tile");
   static_assert(LDS <= 163840, "LDS budget");
 };
@@ -63,10 +67,10 @@ template <class K>
 struct Nbr {
   int base[K::NT];
   uint32_t mask[K::NT];
-  __device__ __forceinline__ void init(int r) {
+  __device__ __forceinline__ void init(int r, int mg) {
 #pragma unroll
     for (int t = 0; t < K::NT; ++t) {
-      const int row = t * 32 + r;
+      const int row = (mg * K::NT + t) * 32 + r;
       base[t] = row * K::RS;
       uint32_t m = 0;
       if (row < K::VROWS) {
@@ -87,29 +91,70 @@ struct Nbr {
   }
 };
 
-template <class K, int KK, int TAPS, bool RESID>
-__device__ __forceinline__ void conv_layer(const char *src, char *dst, const Nbr<K> &nb, const bf16x8 *w,
-                                           const float *bias, int wave, int lane) {
-  constexpr int STEPS = TAPS * KK;
-  constexpr int DEPTH = (KK % 4 == 0) ? 4 : 1;
+// Accumulator initialisation: bias (and, for the second conv of a block, the residual input,
+// which lives at the output location in dst) so the epilogue is only ReLU + bf16 + store.
+template <class K, bool RESID>
+__device__ __forceinline__ void acc_init(f32x16 (&acc)[K::MT][K::NT], const char *dst, const float *bias, int wave,
+                                         int lane) {
   const int r = lane & 31, h = lane >> 5;
-  f32x16 acc[K::MT][K::NT];
 #pragma unroll
   for (int m = 0; m < K::MT; ++m)
 #pragma unroll
-    for (int t = 0; t < K::NT; ++t)
+    for (int g = 0; g < 4; ++g) {
+      const int ch = ((wave % K::CG) * K::MT + m) * 32 + 8 * g + 4 * h;
+      const float4 bv = *(const float4 *)(bias + ch);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[m][t][i] = 0.f;
+      for (int t = 0; t < K::NT; ++t) {
+        float v0 = bv.x, v1 = bv.y, v2 = bv.z, v3 = bv.w;
+        if (RESID) {
+          const bf16x4 x = *(const bf16x4 *)(dst + (((wave / K::CG) * K::NT + t) * 32 + r) * K::RS + ch * 2);
+          v0 += (float)x[0];
+          v1 += (float)x[1];
+          v2 += (float)x[2];
+          v3 += (float)x[3];
+        }
+        acc[m][t][4 * g + 0] = v0;
+        acc[m][t][4 * g + 1] = v1;
+        acc[m][t][4 * g + 2] = v2;
+        acc[m][t][4 * g + 3] = v3;
+      }
+    }
+}
 
-  // weight fragment of (ctile, step s): w[(ct * STEPS + s) * 64 + lane]
-  const bf16x8 *wl[K::MT];
+template <class K>
+__device__ __forceinline__ void acc_store_relu(const f32x16 (&acc)[K::MT][K::NT], char *dst, int wave, int lane) {
+  const int r = lane & 31, h = lane >> 5;
 #pragma unroll
-  for (int m = 0; m < K::MT; ++m) wl[m] = w + (size_t)(wave * K::MT + m) * STEPS * 64 + lane;
-  bf16x8 a[DEPTH][K::MT];
+  for (int m = 0; m < K::MT; ++m)
 #pragma unroll
-  for (int d = 0; d < DEPTH; ++d)
+    for (int g = 0; g < 4; ++g) {
+      const int ch = ((wave % K::CG) * K::MT + m) * 32 + 8 * g + 4 * h;
 #pragma unroll
-    for (int m = 0; m < K::MT; ++m) a[d][m] = wl[m][(size_t)d * 64];
+      for (int t = 0; t < K::NT; ++t) {
+        bf16x4 o;
+        o[0] = (__bf16)fmaxf(acc[m][t][4 * g + 0], 0.f);
+        o[1] = (__bf16)fmaxf(acc[m][t][4 * g + 1], 0.f);
+        o[2] = (__bf16)fmaxf(acc[m][t][4 * g + 2], 0.f);
+        o[3] = (__bf16)fmaxf(acc[m][t][4 * g + 3], 0.f);
+        *(bf16x4 *)(dst + (((wave / K::CG) * K::NT + t) * 32 + r) * K::RS + ch * 2) = o;
+      }
+    }
+}
+
+// One 3x3 conv layer over the resident tile: src (LDS) -> dst (LDS); RESID adds dst's old
+// contents (the block input).  KK = input channels / 16 (k-steps per tap).
+// Software pipeline: the NT B (activation) fragments of step s+1 are read from LDS while the
+// MFMAs of step s run; the A (weight) fragment ring runs DEPTH steps ahead and continues into
+// the next layer's weights (wn), so a layer starts with its first weights already in registers.
+template <class K, int KK, int DEPTH, bool RESID>
+__device__ __forceinline__ void conv_layer(const char *src, char *dst, const Nbr<K> &nb, const bf16x8 *const (&wl)[K::MT],
+                                           const bf16x8 *const (&wn)[K::MT], int wn_steps, bf16x8 (&a)[DEPTH][K::MT],
+                                           const float *bias, int wave, int lane) {
+  constexpr int STEPS = 9 * KK;
+  static_assert(KK % DEPTH == 0, "ring slot must be a compile-time function of kk");
+  const int h = lane >> 5;
+  f32x16 acc[K::MT][K::NT];
+  acc_init<K, RESID>(acc, dst, bias, wave, lane);
 
   const int hoff = 16 * h;  // byte offset of this lane's 8 channels inside a 16-channel k-step
   int off_cur[K::NT], off_nxt[K::NT];
@@ -119,30 +164,32 @@ __device__ __forceinline__ void conv_layer(const char *src, char *dst, const Nbr
 #pragma unroll
   for (int t = 0; t < K::NT; ++t) bc[t] = lds_b128(src + off_cur[t]);
 
-  for (int tap = 0; tap < TAPS; ++tap) {
-    if (tap + 1 < TAPS) {
+  for (int tap = 0; tap < 9; ++tap) {
+    if (tap + 1 < 9) {
 #pragma unroll
       for (int t = 0; t < K::NT; ++t) off_nxt[t] = nb.off(t, tap + 1) + hoff;
     }
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
       const int s = tap * KK + kk;
-      // B fragments of step s + 1
       if (kk + 1 < KK) {
 #pragma unroll
         for (int t = 0; t < K::NT; ++t) bn[t] = lds_b128(src + off_cur[t] + (kk + 1) * 32);
-      } else if (tap + 1 < TAPS) {
+      } else if (tap + 1 < 9) {
 #pragma unroll
         for (int t = 0; t < K::NT; ++t) bn[t] = lds_b128(src + off_nxt[t]);
       }
-      const int slot = DEPTH == 1 ? 0 : (kk % DEPTH);
+      const int slot = kk % DEPTH;
       bf16x8 acur[K::MT];
 #pragma unroll
       for (int m = 0; m < K::MT; ++m) acur[m] = a[slot][m];
-      // A fragment of step s + DEPTH
-      if (s + DEPTH < STEPS) {
+      const int sn = s + DEPTH;
+      if (sn < STEPS) {
 #pragma unroll
-        for (int m = 0; m < K::MT; ++m) a[slot][m] = wl[m][(size_t)(s + DEPTH) * 64];
+        for (int m = 0; m < K::MT; ++m) a[slot][m] = wl[m][(size_t)sn * 64];
+      } else if (sn - STEPS < wn_steps) {
+#pragma unroll
+        for (int m = 0; m < K::MT; ++m) a[slot][m] = wn[m][(size_t)(sn - STEPS) * 64];
       }
       // keep the prefetches ahead of this step's MFMAs (hipcc otherwise sinks them just-in-time)
       __builtin_amdgcn_sched_barrier(0);
@@ -158,35 +205,32 @@ __device__ __forceinline__ void conv_layer(const char *src, char *dst, const Nbr
 #pragma unroll
     for (int t = 0; t < K::NT; ++t) off_cur[t] = off_nxt[t];
   }
-  // epilogue: bias (+ residual) + ReLU -> bf16 rows of dst
+  acc_store_relu<K>(acc, dst, wave, lane);
+}
+
+// Stem: 3 input planes padded to one 16-channel k-step per tap (9 steps, weights loaded in place).
+template <class K>
+__device__ __forceinline__ void stem_layer(const char *src, char *dst, const Nbr<K> &nb, const bf16x8 *w,
+                                           const float *bias, int wave, int lane) {
+  const int h = lane >> 5;
+  f32x16 acc[K::MT][K::NT];
+  acc_init<K, false>(acc, dst, bias, wave, lane);
+  bf16x8 a[9][K::MT];
 #pragma unroll
-  for (int m = 0; m < K::MT; ++m) {
+  for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int ch = (wave * K::MT + m) * 32 + 8 * g + 4 * h;
-      const float4 bv = *(const float4 *)(bias + ch);
+    for (int m = 0; m < K::MT; ++m) a[tap][m] = w[((size_t)((wave % K::CG) * K::MT + m) * 9 + tap) * 64 + lane];
 #pragma unroll
-      for (int t = 0; t < K::NT; ++t) {
-        const int cell = t * 32 + r;
-        char *p = dst + cell * K::RS + ch * 2;
-        float v0 = acc[m][t][4 * g + 0] + bv.x, v1 = acc[m][t][4 * g + 1] + bv.y;
-        float v2 = acc[m][t][4 * g + 2] + bv.z, v3 = acc[m][t][4 * g + 3] + bv.w;
-        if (RESID) {
-          const bf16x4 x = *(const bf16x4 *)p;
-          v0 += (float)x[0];
-          v1 += (float)x[1];
-          v2 += (float)x[2];
-          v3 += (float)x[3];
-        }
-        bf16x4 o;
-        o[0] = (__bf16)fmaxf(v0, 0.f);
-        o[1] = (__bf16)fmaxf(v1, 0.f);
-        o[2] = (__bf16)fmaxf(v2, 0.f);
-        o[3] = (__bf16)fmaxf(v3, 0.f);
-        *(bf16x4 *)p = o;
-      }
+  for (int tap = 0; tap < 9; ++tap) {
+#pragma unroll
+    for (int t = 0; t < K::NT; ++t) {
+      const bf16x8 b = lds_b128(src + nb.off(t, tap) + 16 * h);
+#pragma unroll
+      for (int m = 0; m < K::MT; ++m)
+        acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[tap][m], b, acc[m][t], 0, 0, 0);
     }
   }
+  acc_store_relu<K>(acc, dst, wave, lane);
 }
 
 // 1x1 head convs (C -> C/4 policy | C/4 value) + bias + ReLU, to global features
@@ -196,8 +240,9 @@ __device__ __forceinline__ void head_layer(const char *src, const bf16x8 *w, con
                                            int board0, int batch, int wave, int lane) {
   constexpr int KK = K::C / 16;
   constexpr int GROUPS = 4 / K::HCT;       // waves sharing one head channel tile
-  constexpr int TPW = K::NT / GROUPS;      // cell tiles per wave
-  static_assert(K::HCT * GROUPS == 4 && TPW * GROUPS == K::NT, "head tile plan");
+  constexpr int TILES = K::ROWS / 32;      // all cell tiles of the workgroup
+  constexpr int TPW = TILES / GROUPS;      // cell tiles per wave
+  static_assert(K::HCT * GROUPS == 4 && TPW * GROUPS == TILES, "head tile plan");
   const int r = lane & 31, h = lane >> 5;
   const int ct = wave % K::HCT;
   const int t0 = (wave / K::HCT) * TPW;
@@ -253,7 +298,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int board0 = blockIdx.x * K::BOARDS;
   Nbr<K> nb;
-  nb.init(lane & 31);
+  nb.init(lane & 31, wave / K::CG);
 
   // zero rows + stem input: Y rows hold 16 channels (3 planes, 13 zeros)
   for (int i = tid; i < K::RS / 4; i += 256) {
@@ -270,22 +315,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   __syncthreads();
 
-  const bf16x8 *w = wpk;
-  const float *b = bias;
-  conv_layer<K, 1, 9, false>(Y, X, nb, w, b, wave, lane);
-  w += (size_t)K::C / 32 * 9 * 1 * 64;
-  b += K::C;
+  constexpr int KK = K::C / 16;
+  constexpr int DEPTH = 4;
+  constexpr size_t STEM = (size_t)K::C / 32 * 9 * 64;          // stem fragments
+  constexpr size_t LAYER = (size_t)K::C / 32 * 9 * KK * 64;     // one block conv's fragments
+  constexpr int LSTEPS = 9 * KK;
+  stem_layer<K>(Y, X, nb, wpk, bias, wave, lane);
   __syncthreads();
-  for (int blk = 0; blk < n_blocks; ++blk) {
-    conv_layer<K, K::C / 16, 9, false>(X, Y, nb, w, b, wave, lane);
-    w += (size_t)K::C / 32 * 9 * (K::C / 16) * 64;
-    b += K::C;
-    __syncthreads();
-    conv_layer<K, K::C / 16, 9, true>(Y, X, nb, w, b, wave, lane);
-    w += (size_t)K::C / 32 * 9 * (K::C / 16) * 64;
+  const bf16x8 *wblk = wpk + STEM;
+  const float *b = bias + K::C;
+  // per-wave weight streams: layer L, ctile (wave*MT + m) starts at wblk + L*LAYER + ct*LSTEPS*64 + lane
+  bf16x8 ring[DEPTH][K::MT];
+  const int n_convs = 2 * n_blocks;
+  if (n_convs > 0) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d)
+#pragma unroll
+      for (int m = 0; m < K::MT; ++m)
+        ring[d][m] = wblk[(size_t)((wave % K::CG) * K::MT + m) * LSTEPS * 64 + (size_t)d * 64 + lane];
+  }
+  for (int L = 0; L < n_convs; ++L) {
+    const bf16x8 *wl[K::MT], *wn[K::MT];
+#pragma unroll
+    for (int m = 0; m < K::MT; ++m) {
+      const size_t ct = (size_t)((wave % K::CG) * K::MT + m) * LSTEPS * 64 + lane;
+      wl[m] = wblk + (size_t)L * LAYER + ct;
+      wn[m] = wblk + (size_t)(L + 1) * LAYER + ct;
+    }
+    const int wn_steps = L + 1 < n_convs ? LSTEPS : 0;
+    if ((L & 1) == 0)
+      conv_layer<K, KK, DEPTH, false>(X, Y, nb, wl, wn, wn_steps, ring, b, wave, lane);
+    else
+      conv_layer<K, KK, DEPTH, true>(Y, X, nb, wl, wn, wn_steps, ring, b, wave, lane);
     b += K::C;
     __syncthreads();
   }
+  const bf16x8 *w = wblk + (size_t)n_convs * LAYER;
   head_layer<K>(X, w, b, out, board0, batch, wave, lane);
 }
 
@@ -433,6 +498,36 @@ static int launch(const void *planes, int batch, int n_blocks, const void *w, co
   return hipGetLastError() == hipSuccess ? 0 : -11;
 }
 
+static int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+// Full-size workgroups (one per CU, BOARDS boards each) for whole rounds of the chip, then the
+// remainder with half-size workgroups (half the boards, half the time) when it fits in half a
+// round: a batch of 3,800 boards costs 2.5 workgroup-rounds instead of 3.
+template <class KF, class KH>
+static int launch_split(const char *planes, int batch, int n_blocks, const void *w, const float *b, char *out,
+                        hipStream_t s) {
+  const int cus = num_cus();
+  const int full_wgs = (batch / KF::BOARDS) / cus * cus;
+  const int n_full = full_wgs * KF::BOARDS;
+  const int rem = batch - n_full;
+  int rc = 0;
+  if (n_full > 0) rc = launch<KF>(planes, n_full, n_blocks, w, b, out, s);
+  if (rc || rem <= 0) return rc;
+  const char *p2 = planes + (size_t)n_full * KF::CELLS * 3 * 2;
+  char *o2 = out + (size_t)n_full * KF::CELLS * KF::HEAD * 2;
+  if (rem <= cus * KH::BOARDS) return launch<KH>(p2, rem, n_blocks, w, b, o2, s);
+  return launch<KF>(p2, rem, n_blocks, w, b, o2, s);
+}
+
 }  // namespace tower
 
 extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t channels, int32_t n_blocks,
@@ -441,10 +536,25 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
   using namespace tower;
   hipStream_t s = (hipStream_t)stream;
   if (n_blocks < 0 || batch < 0) return -3;
-  if (width == 7 && height == 6 && channels == 128)
-    return launch<Cfg<128, 256, 7, 6>>(planes_dev, batch, n_blocks, weights_dev, bias_dev, features_dev, s);
+  static int cg = -1;
+  if (cg < 0) {
+    const char *e = getenv("SPMCTS_TOWER_CG");  // A/B switch for the wave split (2 = default)
+    cg = e ? atoi(e) : 2;
+  }
+  const char *pl = (const char *)planes_dev;
+  char *ft = (char *)features_dev;
+  if (width == 7 && height == 6 && channels == 128) {
+    switch (cg) {
+      case 1: return launch<Cfg<128, 256, 7, 6, 1>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      case 4: return launch<Cfg<128, 256, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      case 3: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      case 5: return launch<Cfg<128, 256, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      default: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+    }
+  }
   if (width == 7 && height == 6 && channels == 256)
-    return launch<Cfg<256, 128, 7, 6>>(planes_dev, batch, n_blocks, weights_dev, bias_dev, features_dev, s);
+    return cg == 2 ? launch<Cfg<256, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s)
+                   : launch<Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
   if (width == 3 && height == 3 && channels == 128)
     return launch<Cfg<128, 256, 3, 3>>(planes_dev, batch, n_blocks, weights_dev, bias_dev, features_dev, s);
   if (width == 3 && height == 3 && channels == 256)
