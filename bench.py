@@ -40,6 +40,11 @@ def resnet_flops_per_leaf(W, H, A, filter_factor, num_blocks):
     return f
 
 
+def head_linear_flops(W, H, A, filter_factor):
+    ff, cells = filter_factor, W * H
+    return 2 * ff * cells * A + 2 * ff * cells * 8 * ff + 2 * 8 * ff
+
+
 def select_bytes(sims, levels, A=7):
     """Algorithmic HBM bytes moved by k_select.
 
@@ -140,7 +145,6 @@ def main():
     eng.check()
     c0 = eng.counters()
     eng.enable_timers(True)
-    rows0, pad0 = eng.nn_rows, eng.nn_rows_padded
 
     D.barrier()
     torch.cuda.synchronize()
@@ -170,10 +174,17 @@ def main():
 
     # ---- network (MFMA) share
     nn_ms = eng.nn_timer.total_ms()
-    rows = eng.nn_rows - rows0
-    rows_padded = eng.nn_rows_padded - pad0
+    rows = c1["nn_leaves"] - c0["nn_leaves"]
     fpl = resnet_flops_per_leaf(7, 6, 7, args.filter_factor, args.blocks)
     nn_tflops = rows * fpl / (nn_ms / 1e3) / 1e12 if nn_ms > 0 else 0.0
+    # ---- dominant kernel: k_tower (HIP events around each tower launch on the arena's stream)
+    tw = eng.tower_timer
+    tw_ms = tw.total_ms() if tw is not None and tw.count() else 0.0
+    tw_launches = tw.count() if tw is not None else 0
+    trunk_fpl = fpl - head_linear_flops(7, 6, 7, args.filter_factor)
+    tw_flops_per_launch = rows * trunk_fpl / max(1, tw_launches)
+    tw_avg_s = tw_ms / 1e3 / max(1, tw_launches)
+    tw_tflops = tw_flops_per_launch / tw_avg_s / 1e12 if tw_avg_s > 0 else 0.0
 
     out = {
         "metric": "self-play positions/sec (Connect4, 200 sims/move)",
@@ -198,6 +209,19 @@ def main():
             "parallelism": f"dp{world}",
         },
         "roofline": {
+            "kernel": "tower::k_tower_dyn (fused ResNet-128x20 trunk, bf16 MFMA)",
+            "bound": "mfma",
+            "achieved": tw_tflops,
+            "peak": BF16_DENSE_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": tw_tflops / BF16_DENSE_PEAK_TFLOPS,
+            "traffic": None,
+            "flops_per_launch": tw_flops_per_launch,
+            "flops_per_leaf": trunk_fpl,
+            "avg_launch_us": tw_avg_s * 1e6,
+            "launches": tw_launches,
+        },
+        "tree_roofline": {
             "kernel": "k_select<C4> (PUCT tree walk)",
             "bound": "hbm",
             "achieved": achieved,
@@ -216,7 +240,6 @@ def main():
             "frac": nn_tflops / BF16_DENSE_PEAK_TFLOPS,
             "flops_per_leaf": fpl,
             "rows": rows,
-            "rows_padded": rows_padded,
             "nn_ms": nn_ms,
             "share_of_step": nn_ms / 1e3 / elapsed if elapsed else None,
         },

@@ -229,6 +229,14 @@ int spmcts_tower_heads(int32_t width, int32_t height, int32_t channels, int32_t 
 int spmcts_head_epilogue(int32_t hidden, int32_t actions, const void *z_dev, int32_t ldz, int32_t batch,
                          const float *head_b_dev, float *probs_dev, float *values_dev, spmcts_stream stream);
 int spmcts_tower_supported(int32_t width, int32_t height, int32_t channels);
+/* Device-count variants: the batch size is read from count_dev (e.g. the leaf-row count written by
+ * spmcts_select) so no host synchronisation is needed; max_batch bounds the grid. */
+int spmcts_tower_forward_dev(int32_t width, int32_t height, int32_t channels, int32_t n_blocks, const void *planes_dev,
+                             const int32_t *count_dev, int32_t max_batch, const void *weights_dev,
+                             const float *bias_dev, void *features_dev, spmcts_stream stream);
+int spmcts_tower_heads_dev(int32_t width, int32_t height, int32_t channels, int32_t actions, const void *features_dev,
+                           const int32_t *count_dev, int32_t max_batch, const void *head_w_dev,
+                           const float *head_b_dev, float *probs_dev, float *values_dev, spmcts_stream stream);
 /* Memory-roofline helper: device copy bandwidth probe (bytes each way). */
 int spmcts_copy_probe(const void *src_dev, void *dst_dev, uint64_t bytes, spmcts_stream stream);
 

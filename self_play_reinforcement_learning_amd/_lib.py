@@ -115,6 +115,8 @@ _SIGS = {
     "spmcts_tower_supported": [_I32, _I32, _I32],
     "spmcts_tower_heads": [_I32, _I32, _I32, _I32, _P, _I32, _P, _P, _P, _P, _P],
     "spmcts_head_epilogue": [_I32, _I32, _P, _I32, _I32, _P, _P, _P, _P],
+    "spmcts_tower_forward_dev": [_I32, _I32, _I32, _I32, _P, _P, _I32, _P, _P, _P, _P],
+    "spmcts_tower_heads_dev": [_I32, _I32, _I32, _I32, _P, _P, _I32, _P, _P, _P, _P, _P],
 }
 
 # every symbol the header declares (tests check the .so exports exactly these)

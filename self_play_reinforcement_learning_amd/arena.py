@@ -173,6 +173,24 @@ class Arena:
             call("spmcts_leaf_rows", self.h, ptr(self._leaves), ptr(self._count), _stream())
         return self._read_count()
 
+    def select_async(self, timer=None):
+        """select() without reading the row count back (for device-count evaluators)."""
+        if timer is None:
+            call("spmcts_select", self.h, ptr(self._leaves), ptr(self._count), _stream())
+        else:
+            timer.start()
+            call("spmcts_select_tree", self.h, _stream())
+            timer.stop()
+            call("spmcts_leaf_rows", self.h, ptr(self._leaves), ptr(self._count), _stream())
+
+    def games_end_ply_async(self):
+        call("spmcts_games_end_ply", self.h, ptr(self._leaves), ptr(self._count), _stream())
+
+    @property
+    def count_dev(self):
+        """Device int32 holding the row count of the last select / play_action / games_end_ply."""
+        return self._count
+
     def expand(self, probs, values):
         probs = probs.float().contiguous()
         values = values.float().reshape(-1).contiguous()

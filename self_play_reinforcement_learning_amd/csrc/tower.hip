@@ -32,11 +32,12 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 
-template <int C_, int ROWS_, int W_, int H_, int CG_ = 2>
+template <int C_, int ROWS_, int W_, int H_, int CG_ = 2, int WAVES_ = 4>
 struct Cfg {
   static constexpr int C = C_, ROWS = ROWS_, W = W_, H = H_;
-  static constexpr int CG = CG_;        // waves split output channels into CG groups ...
-  static constexpr int MG = 4 / CG_;    // ... and cell rows into MG groups (4 waves)
+  static constexpr int WAVES = WAVES_, THREADS = 64 * WAVES_;
+  static constexpr int CG = CG_;            // waves split output channels into CG groups ...
+  static constexpr int MG = WAVES_ / CG_;   // ... and cell rows into MG groups
   static constexpr int CELLS = W * H;
   static constexpr int BOARDS = ROWS / CELLS;
   static constexpr int VROWS = BOARDS * CELLS;
@@ -49,7 +50,7 @@ struct Cfg {
   static constexpr int HEAD = C / 2;  // policy filter_factor | value filter_factor channels (filter_factor = C/4)
   static constexpr int HCT = HEAD / 32;  // head channel tiles
   static_assert(MT >= 1 && NT >= 1 && MT * NT <= 8, "tile plan: at most 8 accumulator tiles per wave");
-  static_assert(CG * MG == 4, "4 waves");
+  static_assert(CG * MG == WAVES, "wave plan");
   static_assert(BOARDS >= 1, "board larger than a tile");
   static_assert(LDS <= 163840, "LDS budget");
 };
@@ -239,10 +240,10 @@ template <class K>
 __device__ __forceinline__ void head_layer(const char *src, const bf16x8 *w, const float *bias, __bf16 *out,
                                            int board0, int batch, int wave, int lane) {
   constexpr int KK = K::C / 16;
-  constexpr int GROUPS = 4 / K::HCT;       // waves sharing one head channel tile
+  constexpr int GROUPS = K::WAVES / K::HCT;  // waves sharing one head channel tile
   constexpr int TILES = K::ROWS / 32;      // all cell tiles of the workgroup
   constexpr int TPW = TILES / GROUPS;      // cell tiles per wave
-  static_assert(K::HCT * GROUPS == 4 && TPW * GROUPS == TILES, "head tile plan");
+  static_assert(K::HCT * GROUPS == K::WAVES && TPW * GROUPS == TILES, "head tile plan");
   const int r = lane & 31, h = lane >> 5;
   const int ct = wave % K::HCT;
   const int t0 = (wave / K::HCT) * TPW;
@@ -289,23 +290,22 @@ __device__ __forceinline__ void head_layer(const char *src, const bf16x8 *w, con
 //   head   [C/64][1][C/16][64]          policy C/4 | value C/4 output channels
 // lane l of fragment (ct, tap, kk) holds W[ct*32 + (l & 31)][tap][kk*16 + 8*(l >> 5) + j], j = 0..7.
 // bias: stem C, blocks 2*C each, head C/2.
+// One workgroup's tile: boards [board0, board0 + BOARDS) of the batch (board < batch), all layers.
 template <class K>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_tower(const __bf16 *planes, int batch, int n_blocks, const bf16x8 *wpk,
-                                               const float *bias, __bf16 *out) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+__device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int batch, int board0, int n_blocks,
+                                           const bf16x8 *wpk, const float *bias, __bf16 *out) {
   char *X = smem;
   char *Y = smem + K::BUF;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int board0 = blockIdx.x * K::BOARDS;
   Nbr<K> nb;
   nb.init(lane & 31, wave / K::CG);
 
   // zero rows + stem input: Y rows hold 16 channels (3 planes, 13 zeros)
-  for (int i = tid; i < K::RS / 4; i += 256) {
+  for (int i = tid; i < K::RS / 4; i += K::THREADS) {
     ((uint32_t *)(X + K::ZROW * K::RS))[i] = 0u;
     ((uint32_t *)(Y + K::ZROW * K::RS))[i] = 0u;
   }
-  for (int row = tid; row < K::ROWS; row += 256) {
+  for (int row = tid; row < K::ROWS; row += K::THREADS) {
     const int board = board0 + row / K::CELLS;
     __bf16 *dst = (__bf16 *)(Y + row * K::RS);
     const bool ok = row < K::VROWS && board < batch;
@@ -354,6 +354,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   head_layer<K>(X, w, b, out, board0, batch, wave, lane);
 }
 
+template <class K>
+__global__ __launch_bounds__(K::THREADS) __attribute__((amdgpu_waves_per_eu(K::WAVES / 4, K::WAVES / 4))) void k_tower(
+    const __bf16 *planes, int batch, int n_blocks, const bf16x8 *wpk, const float *bias, __bf16 *out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  tower_tile<K>(smem, planes, batch, blockIdx.x * K::BOARDS, n_blocks, wpk, bias, out);
+}
+
+// Device-count driven variant: the batch size is read from device memory (the arena's leaf-row
+// counter), so the host never waits for it.  Workgroups are assigned as in launch_split: whole
+// chip rounds of full-size tiles, then the remainder in half-size tiles when it fits half a round;
+// surplus workgroups of the (maximum-size) grid exit at once.
+template <class KF, class KH>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_tower_dyn(
+    const __bf16 *planes, const int32_t *count, int cus, int n_blocks, const bf16x8 *wpk, const float *bias,
+    __bf16 *out) {
+  static_assert(KF::THREADS == 256 && KH::THREADS == 256, "one block size");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int n = *count;
+  const int full_wgs = (n / KF::BOARDS) / cus * cus;
+  const int n_full = full_wgs * KF::BOARDS;
+  const int rem = n - n_full;
+  const int b = blockIdx.x;
+  if (b < full_wgs) {
+    tower_tile<KF>(smem, planes, n, b * KF::BOARDS, n_blocks, wpk, bias, out);
+    return;
+  }
+  const int j = b - full_wgs;
+  if (rem <= cus * KH::BOARDS) {
+    if (n_full + j * KH::BOARDS < n) tower_tile<KH>(smem, planes, n, n_full + j * KH::BOARDS, n_blocks, wpk, bias, out);
+  } else {
+    if (n_full + j * KF::BOARDS < n) tower_tile<KF>(smem, planes, n, n_full + j * KF::BOARDS, n_blocks, wpk, bias, out);
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Linear heads (modules.py:96-105 after the 1x1 convs), fused: for 32 boards per workgroup
 //   policy = softmax(pf @ Wp^T + bp)          pf = features[:, :, :ff]  (cell-major, K = cells*ff)
@@ -361,8 +395,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 // on v_mfma_f32_32x32x16_bf16 with M = 32 boards.  Weight blob (bf16): Wp padded to 32 rows
 // [32][K] then Wv [8ff][K]; float blob: bp[32] (padded), bv[8ff], wo[8ff], bo.
 template <int FF, int CELLS, int A>
-__global__ __launch_bounds__(256) void k_heads(const __bf16 *feats, int n, const __bf16 *hw, const float *hb,
-                                               float *probs, float *values) {
+__global__ __launch_bounds__(256) void k_heads(const __bf16 *feats, int n, const int32_t *count, const __bf16 *hw,
+                                               const float *hb, float *probs, float *values) {
+  if (count) n = *count;
+  if ((int)blockIdx.x * 32 >= n) return;
   constexpr int K = CELLS * FF;
   constexpr int KS = K / 16;
   constexpr int HID = 8 * FF;
@@ -493,7 +529,7 @@ static int launch(const void *planes, int batch, int n_blocks, const void *w, co
       return -10;
     attr_set = true;
   }
-  hipLaunchKernelGGL(k_tower<K>, dim3(grid), dim3(256), K::LDS, s, (const __bf16 *)planes, batch, n_blocks,
+  hipLaunchKernelGGL(k_tower<K>, dim3(grid), dim3(K::THREADS), K::LDS, s, (const __bf16 *)planes, batch, n_blocks,
                      (const bf16x8 *)w, b, (__bf16 *)out);
   return hipGetLastError() == hipSuccess ? 0 : -11;
 }
@@ -528,7 +564,48 @@ static int launch_split(const char *planes, int batch, int n_blocks, const void 
   return launch<KF>(p2, rem, n_blocks, w, b, o2, s);
 }
 
+template <class KF, class KH>
+static int launch_dyn(const void *planes, const int32_t *count, int max_batch, int n_blocks, const void *w,
+                      const float *b, void *out, hipStream_t s) {
+  const int cus = num_cus();
+  const int grid = (max_batch + KF::BOARDS - 1) / KF::BOARDS + cus;
+  constexpr int LDS = KF::LDS > KH::LDS ? KF::LDS : KH::LDS;
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute((const void *)k_tower_dyn<KF, KH>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS) !=
+        hipSuccess)
+      return -10;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((k_tower_dyn<KF, KH>), dim3(grid), dim3(256), LDS, s, (const __bf16 *)planes, count, cus,
+                     n_blocks, (const bf16x8 *)w, b, (__bf16 *)out);
+  return hipGetLastError() == hipSuccess ? 0 : -11;
+}
+
 }  // namespace tower
+
+extern "C" int spmcts_tower_forward_dev(int32_t width, int32_t height, int32_t channels, int32_t n_blocks,
+                                        const void *planes_dev, const int32_t *count_dev, int32_t max_batch,
+                                        const void *weights_dev, const float *bias_dev, void *features_dev,
+                                        spmcts_stream stream) {
+  using namespace tower;
+  hipStream_t s = (hipStream_t)stream;
+  if (n_blocks < 0 || max_batch < 0 || !count_dev) return -3;
+  if (max_batch == 0) return 0;
+  if (width == 7 && height == 6 && channels == 128)
+    return launch_dyn<Cfg<128, 256, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(planes_dev, count_dev, max_batch, n_blocks,
+                                                                      weights_dev, bias_dev, features_dev, s);
+  if (width == 7 && height == 6 && channels == 256)
+    return launch_dyn<Cfg<256, 128, 7, 6, 4>, Cfg<256, 128, 7, 6, 4>>(planes_dev, count_dev, max_batch, n_blocks,
+                                                                      weights_dev, bias_dev, features_dev, s);
+  if (width == 3 && height == 3 && channels == 128)
+    return launch_dyn<Cfg<128, 256, 3, 3, 2>, Cfg<128, 128, 3, 3, 2>>(planes_dev, count_dev, max_batch, n_blocks,
+                                                                      weights_dev, bias_dev, features_dev, s);
+  if (width == 3 && height == 3 && channels == 256)
+    return launch_dyn<Cfg<256, 128, 3, 3, 4>, Cfg<256, 128, 3, 3, 4>>(planes_dev, count_dev, max_batch, n_blocks,
+                                                                      weights_dev, bias_dev, features_dev, s);
+  return -2;
+}
 
 extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t channels, int32_t n_blocks,
                                     const void *planes_dev, int32_t batch, const void *weights_dev,
@@ -549,12 +626,14 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
       case 4: return launch<Cfg<128, 256, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       case 3: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       case 5: return launch<Cfg<128, 256, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      case 8: return launch_split<Cfg<128, 256, 7, 6, 2, 8>, Cfg<128, 128, 7, 6, 2, 8>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      case 9: return launch_split<Cfg<128, 256, 7, 6, 4, 8>, Cfg<128, 128, 7, 6, 4, 8>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       default: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
     }
   }
   if (width == 7 && height == 6 && channels == 256)
     return cg == 2 ? launch<Cfg<256, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s)
-                   : launch<Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+                   : launch<Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);  // CG=4 default
   if (width == 3 && height == 3 && channels == 128)
     return launch<Cfg<128, 256, 3, 3>>(planes_dev, batch, n_blocks, weights_dev, bias_dev, features_dev, s);
   if (width == 3 && height == 3 && channels == 256)
@@ -562,16 +641,16 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
   return -2;
 }
 
-extern "C" int spmcts_tower_heads(int32_t width, int32_t height, int32_t channels, int32_t actions,
-                                  const void *features_dev, int32_t batch, const void *head_w_dev,
-                                  const float *head_b_dev, float *probs_dev, float *values_dev, spmcts_stream stream) {
+static int tower_heads(int32_t width, int32_t height, int32_t channels, int32_t actions, const void *features_dev,
+                       int32_t batch, const int32_t *count_dev, const void *head_w_dev, const float *head_b_dev,
+                       float *probs_dev, float *values_dev, spmcts_stream stream) {
   using namespace tower;
   hipStream_t s = (hipStream_t)stream;
   if (batch <= 0) return batch < 0 ? -3 : 0;
   const int grid = (batch + 31) / 32;
 #define HEADS(FF, CELLS, A)                                                                                   \
   hipLaunchKernelGGL((k_heads<FF, CELLS, A>), dim3(grid), dim3(256), 0, s, (const __bf16 *)features_dev, batch, \
-                     (const __bf16 *)head_w_dev, head_b_dev, probs_dev, values_dev)
+                     count_dev, (const __bf16 *)head_w_dev, head_b_dev, probs_dev, values_dev)
   if (width == 7 && height == 6 && actions == 7 && channels == 128)
     HEADS(32, 42, 7);
   else if (width == 7 && height == 6 && actions == 7 && channels == 256)
@@ -584,6 +663,21 @@ extern "C" int spmcts_tower_heads(int32_t width, int32_t height, int32_t channel
     return -2;
 #undef HEADS
   return hipGetLastError() == hipSuccess ? 0 : -11;
+}
+
+extern "C" int spmcts_tower_heads(int32_t width, int32_t height, int32_t channels, int32_t actions,
+                                  const void *features_dev, int32_t batch, const void *head_w_dev,
+                                  const float *head_b_dev, float *probs_dev, float *values_dev, spmcts_stream stream) {
+  return tower_heads(width, height, channels, actions, features_dev, batch, nullptr, head_w_dev, head_b_dev, probs_dev,
+                     values_dev, stream);
+}
+
+extern "C" int spmcts_tower_heads_dev(int32_t width, int32_t height, int32_t channels, int32_t actions,
+                                      const void *features_dev, const int32_t *count_dev, int32_t max_batch,
+                                      const void *head_w_dev, const float *head_b_dev, float *probs_dev,
+                                      float *values_dev, spmcts_stream stream) {
+  return tower_heads(width, height, channels, actions, features_dev, max_batch, count_dev, head_w_dev, head_b_dev,
+                     probs_dev, values_dev, stream);
 }
 
 extern "C" int spmcts_head_epilogue(int32_t hidden, int32_t actions, const void *z_dev, int32_t ldz, int32_t batch,

@@ -83,6 +83,7 @@ class SelfPlayEngine:
         self.started = False
         self.select_timer = None
         self.nn_timer = None
+        self.async_device = True  # device-count evaluators run a whole ply without host syncs
         self.refresh_root_prior()
 
     @torch.no_grad()
@@ -101,6 +102,8 @@ class SelfPlayEngine:
     def enable_timers(self, on=True):
         self.select_timer = EventTimer() if on else None
         self.nn_timer = EventTimer() if on else None
+        self.tower_timer = EventTimer() if on else None
+        self.evaluator.tower_timer = self.tower_timer
 
     def start(self):
         """Fill every slot and keep refilling (until `max_games` games have started, if set)."""
@@ -125,15 +128,32 @@ class SelfPlayEngine:
         self.nn_rows += n
         self.nn_rows_padded += m
 
+    def _eval_expand_dev(self):
+        """Network + expand on the device-side row count: no host synchronisation."""
+        a = self.arena
+        if self.nn_timer is not None:
+            self.nn_timer.start()
+        probs, values = self.evaluator.forward_dev(a.leaves(a.max_rows), a.count_dev, a.max_rows)
+        if self.nn_timer is not None:
+            self.nn_timer.stop()
+        a.expand(probs, values)
+
     def ply(self, on_moves=None, refill=True):
         """Advance every active game by one move. Returns (#games finished, #records exported)."""
         if not self.started:
             self.start()
         a = self.arena
         a.games_begin_ply()
-        for _ in range(self.iterations):
-            self._eval_expand(a.select(self.select_timer))
-        self._eval_expand(a.games_end_ply())
+        if getattr(self.evaluator, "supports_device_count", False) and self.async_device:
+            for _ in range(self.iterations):
+                a.select_async(self.select_timer)
+                self._eval_expand_dev()
+            a.games_end_ply_async()
+            self._eval_expand_dev()
+        else:
+            for _ in range(self.iterations):
+                self._eval_expand(a.select(self.select_timer))
+            self._eval_expand(a.games_end_ply())
         finished, ring = a.games_finish_ply(refill=refill)
         exported = 0
         if ring:

@@ -272,6 +272,43 @@ class HipTowerEvaluator(Evaluator):
                                 t.linear_policy.bias.detach().float()]).to(dev).contiguous()
         t.train(was)
 
+    supports_device_count = True
+
+    @torch.no_grad()
+    def forward_dev(self, leaves, count_dev, max_rows):
+        """Evaluate the first *count_dev rows of `leaves` without a host synchronisation.
+
+        leaves: the arena's whole leaf buffer (NCHW view of NHWC bf16 storage, >= max_rows rows);
+        count_dev: device int32 holding the row count.  Returns max_rows-row probs/values buffers
+        of which the first *count_dev rows are valid (the arena's expand reads the same count)."""
+        dev = leaves.device
+        buf = getattr(self, "_dev_bufs", None)
+        if buf is None or buf[0].shape[0] < max_rows or buf[0].device != dev:
+            buf = (torch.empty((max_rows, self.cells, self.C // 2), dtype=torch.bfloat16, device=dev),
+                   torch.empty((max_rows, self.A), dtype=torch.float32, device=dev),
+                   torch.empty(max_rows, dtype=torch.float32, device=dev))
+            self._dev_bufs = buf
+        feats, probs, values = buf
+        c = self._lib.ctypes.c_void_p
+        stream = c(torch.cuda.current_stream().cuda_stream)
+        L = self._lib.lib()
+        timer = getattr(self, "tower_timer", None)
+        if timer is not None:
+            timer.start()
+        rc = L.spmcts_tower_forward_dev(self.W, self.H, self.C, self.n_blocks, c(leaves.data_ptr()),
+                                        c(count_dev.data_ptr()), max_rows, c(self.wblob.data_ptr()),
+                                        c(self.bblob.data_ptr()), c(feats.data_ptr()), stream)
+        if timer is not None:
+            timer.stop()
+        if rc != 0:
+            raise self._lib.SpmctsError(f"spmcts_tower_forward_dev failed ({rc})")
+        rc = L.spmcts_tower_heads_dev(self.W, self.H, self.C, self.A, c(feats.data_ptr()), c(count_dev.data_ptr()),
+                                      max_rows, c(self.head_w.data_ptr()), c(self.head_b.data_ptr()),
+                                      c(probs.data_ptr()), c(values.data_ptr()), stream)
+        if rc != 0:
+            raise self._lib.SpmctsError(f"spmcts_tower_heads_dev failed ({rc})")
+        return probs, values
+
     @torch.no_grad()
     def trunk(self, planes_nhwc):
         """planes: bf16 [n, W, H, 3] contiguous -> head features bf16 [n, cells, C/2]."""
