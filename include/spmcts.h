@@ -54,6 +54,12 @@ enum spmcts_leaf_format {
   SPMCTS_LEAF_BOARD_I64 = 3 /* int64 boards [B,W,H] = state * mover, for net.forward(s)        */
 };
 enum spmcts_layout { SPMCTS_NCHW = 0, SPMCTS_NHWC = 1 };
+/* What plays a tree's moves in games mode (games/general/hardcoded_players.py) */
+enum spmcts_player_kind {
+  SPMCTS_PLAYER_MCTS = 0,     /* MCTreeSearch (the default)                                 */
+  SPMCTS_PLAYER_RANDOM = 1,   /* Random: uniform over valid moves (hardcoded_players.py:36-56) */
+  SPMCTS_PLAYER_LOOKAHEAD = 2 /* OneStepLookahead: win / block / random (:8-33)               */
+};
 
 /* device error flags (sticky) */
 #define SPMCTS_ERR_POOL 0x1u      /* a tree ran out of node blocks                 */
@@ -131,7 +137,9 @@ int spmcts_tree_reset(spmcts_arena *h, const int32_t *trees_dev, const int8_t *r
 int spmcts_search_begin(spmcts_arena *h, const int32_t *trees_dev, int32_t n, spmcts_stream stream);
 /* One search_node (mcts.py:340-367) for every active tree: PUCT select with
  * jitter, terminal leaves backed up in place, other leaves written to the leaf
- * batch (rows in tree order).  *leaf_count_dev = rows written. */
+ * batch (rows in tree order).  leaf_count_dev int32[3] = {rows, network-0 rows,
+ * network-1 rows}: network-0 leaves occupy rows [0, n0), network-1 leaves rows
+ * [seg1, seg1 + n1) (see spmcts_set_tree_players; single-network arenas: n1 = 0). */
 int spmcts_select(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_dev, spmcts_stream stream);
 /* spmcts_select in two launches (for per-kernel timing): the tree walk alone,
  * then the leaf-row compaction + encode of whatever is pending. */
@@ -142,6 +150,21 @@ int spmcts_leaf_rows(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_dev,
  * back the value up the path.  probs_dev [rows][A] f32, values_dev [rows] f32
  * (network outputs from the mover's perspective, modules.py:109-112). */
 int spmcts_expand(spmcts_arena *h, const float *probs_dev, const float *values_dev, spmcts_stream stream);
+/* Two-network arenas: network-0 outputs indexed by row, network-1 outputs by row - seg1. */
+int spmcts_expand2(spmcts_arena *h, const float *probs0_dev, const float *values0_dev, const float *probs1_dev,
+                   const float *values1_dev, spmcts_stream stream);
+/* (sync) Per-tree players, for evaluation games between two networks or against a
+ * hard-coded player (SelfPlayWorker.set_up_policies evaluate=True, selfplayworker.py:68-94;
+ * compare_models, self_play_parallel.py:355-379).  Host arrays of n_trees entries, each
+ * may be NULL (default): nets = network id 0/1 of the tree's leaves; kinds = enum
+ * spmcts_player_kind; budgets = simulations per search (MCTreeSearch.iterations of that
+ * player; < 0 = unlimited).  Network-1 leaves are placed from row seg1 = #network-0 trees. */
+int spmcts_set_tree_players(spmcts_arena *h, const uint8_t *nets, const uint8_t *kinds, const int32_t *budgets);
+int spmcts_arena_segments(const spmcts_arena *h, int32_t *seg1);
+/* Empty-board root prior of network `net` (0 / 1), used by resets of that network's trees. */
+int spmcts_set_root_prior_net(spmcts_arena *h, int32_t net, const float *probs_dev, spmcts_stream stream);
+/* Games mode: keep Move records (play_episode update=True, the default) or not (evaluation games). */
+int spmcts_games_set_record(spmcts_arena *h, int32_t record);
 /* MCTreeSearch._play (mcts.py:272-299) for the active trees + remove_noise:
  * visit-count^(1/temp) distribution, np.random.choice semantics, Move record.
  * Outputs per active tree i: actions_dev[i], states_dev[i][W*H] (int8, tree

@@ -44,6 +44,9 @@ class NumpyRNG:
     def rand(self, k):
         return np.random.rand(k)
 
+    def choice_index(self, n):
+        raise TypeError("hard-coded players draw from python's `random` (oracle.hardcoded.PyRandomRNG)")
+
     def choice_uniform(self):
         # np.random.choice(a, p=p) with size=None draws exactly one random_sample()
         # after validating p (numpy mtrand.pyx RandomState.choice); see _choice below.
@@ -73,6 +76,9 @@ class TapeRNG:
     def choice_uniform(self):
         return float(self._take(1)[0])
 
+    def choice_index(self, n):  # hard-coded players: floor(u * n) (the arena's form)
+        return min(n - 1, int(float(self._take(1)[0]) * n))
+
 
 class RecordingRNG:
     """Wraps another RNG and records every double it hands out (the HIP tape format)."""
@@ -95,6 +101,11 @@ class RecordingRNG:
         u = self.inner.choice_uniform()
         self.tape.append(float(u))
         return u
+
+    def choice_index(self, n):
+        k = self.inner.choice_index(n)
+        self.tape.append((k + 0.5) / n)
+        return k
 
 
 def _kahan_sum(p):

@@ -8,16 +8,22 @@ owner, selfplayworker.py:175-176, :215-223); both trees advance on every ply
 import numpy as np
 
 from .envs import make_env
+from .hardcoded import HardcodedPlayer
 from .mcts import OracleTree
 
 
 def play_episode(game, net_policy, net_opponent, rng_policy, rng_opponent, iterations, swap_sides=False,
-                 update=True, evaluate=False, alpha=1, strong_play=False, on_ply=None):
+                 update=True, evaluate=False, alpha=1, strong_play=False, on_ply=None, opponent="mcts",
+                 opponent_iterations=None):
     """SelfPlayer.play_episode (selfplayworker.py:172-194).
 
     The reference draws every random number from ONE global RandomState, in
     call order; pass the same NumpyRNG for both trees to reproduce it, or two
     TapeRNG streams (one per tree) to replay a recorded game.
+
+    Evaluation games (set_up_policies(evaluate=True), selfplayworker.py:68-81): the
+    opposing side may be a second network with its own `opponent_iterations`, or
+    opponent="lookahead" / "random" (oracle/hardcoded.py, drawing from rng_opponent).
 
     Returns (result r in the policy's frame, moves pushed to the memory queue in
     push order [policy's then opponent's], per-ply log).
@@ -26,12 +32,26 @@ def play_episode(game, net_policy, net_opponent, rng_policy, rng_opponent, itera
     env.reset()
     pol = OracleTree(game, net_policy, rng_policy, iterations, alpha, strong_play, evaluate=evaluate,
                      root_player=(-1 if swap_sides else 1))
-    opp = OracleTree(game, net_opponent, rng_opponent, iterations, alpha, strong_play, evaluate=evaluate,
-                     root_player=(1 if swap_sides else -1))
+    if opponent == "mcts":
+        opp = OracleTree(game, net_opponent, rng_opponent,
+                         iterations if opponent_iterations is None else opponent_iterations, alpha, strong_play,
+                         evaluate=evaluate, root_player=(1 if swap_sides else -1))
+    else:
+        opp = HardcodedPlayer(opponent, game, rng_opponent)
+        opp.reset(1 if swap_sides else -1)
     log = []
 
     def get_and_play(player):  # :209-219
         tree = pol if player == 1 else opp
+        if isinstance(tree, HardcodedPlayer):
+            a = tree.move()
+            log.append(dict(tree=1, action=a))
+            if on_ply is not None:
+                on_ply(log[-1])
+            pol.play_action(a)
+            opp.play_action(a, -player)  # its own frame (play_move :221-224)
+            _, r, done, _ = env.step(a, player=player)
+            return r * player, done
         tree.search()
         stats = tree.root_stats()
         n_before = len(tree.temp_memory)
@@ -44,7 +64,10 @@ def play_episode(game, net_policy, net_opponent, rng_policy, rng_opponent, itera
             on_ply(log[-1])
         # play_move (:221-224): both trees advance, then the env steps
         pol.play_action(a)
-        opp.play_action(a)
+        if isinstance(opp, HardcodedPlayer):
+            opp.play_action(a, -player)
+        else:
+            opp.play_action(a)
         _, r, done, _ = env.step(a, player=player)
         return r * player, done
 
@@ -61,5 +84,6 @@ def play_episode(game, net_policy, net_opponent, rng_policy, rng_opponent, itera
     moves = []
     if update:
         moves += pol.push_result(r)
-        moves += opp.push_result(-r)
-    return int(r), moves, log, (pol, opp)
+        if not isinstance(opp, HardcodedPlayer):
+            moves += opp.push_result(-r)
+    return int(r), moves, log, (pol, opp, env)

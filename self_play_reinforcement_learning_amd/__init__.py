@@ -8,6 +8,7 @@ Public API mirrors the reference:
     ModelContainer, BasePlayer, Policy    (games/general/base_model.py)
     ResidualTower                         (games/general/modules.py)
     Connect4Env, TicTacToeEnv             (games/connect4, games/tictactoe)
+    OneStepLookahead, Random              (games/general/hardcoded_players.py)
 plus the arena itself: Arena, SelfPlayEngine, DeviceTableNet.
 """
 from .base_model import BasePlayer, ModelContainer, Policy, TrainableModel  # noqa: F401
@@ -25,6 +26,8 @@ _LAZY = {
     "Connect4Env": ".envs",
     "TicTacToeEnv": ".envs",
     "GameOver": ".envs",
+    "OneStepLookahead": ".hardcoded_players",
+    "Random": ".hardcoded_players",
 }
 
 

@@ -15,6 +15,7 @@ CONNECT4, TICTACTOE = 0, 1
 RNG_PHILOX, RNG_TAPE = 0, 1
 LEAF_F32, LEAF_F16, LEAF_BF16, LEAF_BOARD_I64 = 0, 1, 2, 3
 NCHW, NHWC = 0, 1
+PLAYER_MCTS, PLAYER_RANDOM, PLAYER_LOOKAHEAD = 0, 1, 2
 
 ERR_FLAGS = {
     0x1: "node pool exhausted",
@@ -93,6 +94,11 @@ _SIGS = {
     "spmcts_select_tree": [_P, _P],
     "spmcts_leaf_rows": [_P, _P, _P, _P],
     "spmcts_expand": [_P, _P, _P, _P],
+    "spmcts_expand2": [_P, _P, _P, _P, _P, _P],
+    "spmcts_set_tree_players": [_P, _P, _P, _P],
+    "spmcts_arena_segments": [_P, ctypes.POINTER(_I32)],
+    "spmcts_set_root_prior_net": [_P, _I32, _P, _P],
+    "spmcts_games_set_record": [_P, _I32],
     "spmcts_search_end": [_P, _D, _P, _P, _P, _P, _P, _P, _P],
     "spmcts_play_action": [_P, _P, _P, _I32, _P, _P, _P],
     "spmcts_root_stats": [_P, _I32, _P, _P, _P, _P, _P, _P, _P],

@@ -95,6 +95,7 @@ class Arena:
         self._i32 = torch.zeros(rows, dtype=torch.int32, device=dev)
         self._i8 = torch.zeros(rows, dtype=torch.int8, device=dev)
         self.n_active = 0
+        self.seg1 = n_trees  # first leaf row of network 1 (two-network arenas)
         self._L = L
 
     # ------------------------------------------------------------------ lifetime
@@ -123,16 +124,59 @@ class Arena:
             x = x.permute(0, 3, 1, 2)  # NCHW view with channels_last strides
         return x
 
+    def leaves_from(self, row0, n):
+        """Leaf rows [row0, row0 + n) (network-1 rows start at `seg1`)."""
+        x = self._leaves[row0:row0 + n]
+        if self.leaf_format != "board" and self.leaf_layout == "nhwc":
+            x = x.permute(0, 3, 1, 2)
+        return x
+
     def _read_count(self):
         self._count_host.copy_(self._count, non_blocking=True)
         torch.cuda.current_stream().synchronize()
         return int(self._count_host[0])
 
+    def segment_counts(self):
+        """(network-0 rows, network-1 rows) of the last select / play_action / games_end_ply (sync)."""
+        self._count_host.copy_(self._count, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        return int(self._count_host[1]), int(self._count_host[2])
+
     # ------------------------------------------------------------------ configuration
-    def set_root_prior(self, probs):
+    def set_root_prior(self, probs, net=0):
         p = torch.as_tensor(probs, dtype=torch.float32).to(self.device).contiguous()
-        self._root_prior = p
-        call("spmcts_set_root_prior", self.h, ptr(p), _stream())
+        if net == 0:
+            self._root_prior = p
+            call("spmcts_set_root_prior", self.h, ptr(p), _stream())
+        else:
+            self._root_prior1 = p
+            call("spmcts_set_root_prior_net", self.h, int(net), ptr(p), _stream())
+
+    def set_tree_players(self, nets=None, kinds=None, budgets=None):
+        """Per-tree network id (0/1), player kind (_lib.PLAYER_*) and simulations per search.
+
+        Network-1 leaves are written from row `seg1` (= number of network-0 trees) on."""
+        T = self.n_trees
+
+        def arr(x, ctype, dtype):
+            if x is None:
+                return None
+            a = np.ascontiguousarray(np.asarray(x, dtype=dtype))
+            if a.shape != (T,):
+                raise ValueError(f"expected {T} per-tree entries, got {a.shape}")
+            return a.ctypes.data_as(ctypes.POINTER(ctype)), a
+
+        n = arr(nets, ctypes.c_uint8, np.uint8)
+        k = arr(kinds, ctypes.c_uint8, np.uint8)
+        b = arr(budgets, ctypes.c_int32, np.int32)
+        torch.cuda.current_stream().synchronize()
+        call("spmcts_set_tree_players", self.h, n[0] if n else None, k[0] if k else None, b[0] if b else None)
+        seg = ctypes.c_int32()
+        call("spmcts_arena_segments", self.h, ctypes.byref(seg))
+        self.seg1 = seg.value
+
+    def games_set_record(self, record=True):
+        call("spmcts_games_set_record", self.h, int(bool(record)))
 
     def set_tapes(self, tapes):
         """Parity mode: one flat float64 stream per tree (list indexed by tree id)."""
@@ -191,10 +235,20 @@ class Arena:
         """Device int32 holding the row count of the last select / play_action / games_end_ply."""
         return self._count
 
+    def segment_count_dev(self, net):
+        """Device int32 holding network `net`'s row count (element 1 + net of the count buffer)."""
+        return self._count[1 + net:2 + net]
+
     def expand(self, probs, values):
         probs = probs.float().contiguous()
         values = values.float().reshape(-1).contiguous()
         call("spmcts_expand", self.h, ptr(probs), ptr(values), _stream())
+
+    def expand2(self, probs0, values0, probs1, values1):
+        """Two-network expand: network-0 outputs by row, network-1 outputs by row - seg1."""
+        t = [x.float().contiguous() if x.dtype != torch.float32 or not x.is_contiguous() else x
+             for x in (probs0, values0.reshape(-1), probs1, values1.reshape(-1))]
+        call("spmcts_expand2", self.h, *[ptr(x) for x in t], _stream())
 
     def search_end(self, temp=1.0):
         n = self.n_active

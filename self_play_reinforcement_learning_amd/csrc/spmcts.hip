@@ -132,6 +132,13 @@ struct View {
   int32_t ex_cap;
   int64_t *gcnt;  // games counters: [0] finished [1..6] results [7] next id [8] limit [9] exported
   int32_t *gscratch;
+  // per-tree players (two-network arenas, compare_models / evaluation games)
+  uint8_t *tnet;     // [T] network whose leaves this tree sends (0 / 1)
+  uint8_t *tkind;    // [T] SPMCTS_PLAYER_*: MCTS, or a hard-coded player (hardcoded_players.py)
+  int32_t *budget;   // [T] simulations per search of this tree (MCTreeSearch.iterations)
+  int32_t seg1;      // first leaf row of network 1 (= number of network-0 trees)
+  int32_t record;    // games mode: keep Move records (play_episode update=True)
+  int32_t sim;       // index of the current simulation within the search (by value per launch)
 };
 
 enum { C_SIMS = 0, C_NN = 1, C_TERM = 2, C_DEPTH = 3, C_SETNODE = 4, C_MOVES = 5, C_NCNT = 8 };
@@ -296,7 +303,7 @@ __global__ void k_tree_reset(View v, const int32_t *trees, const int8_t *players
     set_err(v, SPMCTS_ERR_STATE);
     return;
   }
-  reset_tree<G>(v, t, players[i], priors ? priors + (size_t)i * G::A : v.root_prior);
+  reset_tree<G>(v, t, players[i], priors ? priors + (size_t)i * G::A : v.root_prior + 16 * v.tnet[t]);
 }
 
 template <class G>
@@ -346,6 +353,7 @@ __global__ __launch_bounds__(64) void k_select(View v, int n_active) {
   if (slot >= n_active) return;
   const int tree = v.active[slot];
   if (tree < 0) return;
+  if (v.sim >= v.budget[tree]) return;  // this tree's search is complete (per-player iterations)
 
   const size_t nb = nbase<G>(v, tree);
   const size_t bb = (size_t)tree * v.cap;
@@ -472,30 +480,50 @@ __global__ __launch_bounds__(64) void k_select(View v, int n_active) {
 // ----------------------------------------------------------------------------
 // kernel: compaction of pending leaves into rows (tree order => deterministic)
 // ----------------------------------------------------------------------------
+// Two segments: leaves of network-0 trees in rows [0, n0), of network-1 trees in rows
+// [seg1, seg1 + n1) (single-network arenas: seg1 = T, n1 = 0).
+// count_out (optional): [0] = n0 + n1, [1] = n0, [2] = n1.
 __global__ __launch_bounds__(1024) void k_scan_need(View v, int32_t *count_out) {
-  __shared__ int32_t s_part[1024];
+  __shared__ int32_t s_p0[1024], s_p1[1024];
   const int tid = threadIdx.x;
   const int T = v.T;
   const int chunk = (T + 1023) / 1024;
   const int lo = min(T, tid * chunk), hi = min(T, lo + chunk);
-  int c = 0;
-  for (int t = lo; t < hi; ++t) c += v.need[t] ? 1 : 0;
-  s_part[tid] = c;
-  __syncthreads();
-  // inclusive Hillis-Steele scan over 1024 partials
-  for (int off = 1; off < 1024; off <<= 1) {
-    const int add = tid >= off ? s_part[tid - off] : 0;
-    __syncthreads();
-    s_part[tid] += add;
-    __syncthreads();
-  }
-  int row = s_part[tid] - c;
+  int c0 = 0, c1 = 0;
   for (int t = lo; t < hi; ++t)
-    if (v.need[t]) v.row_tree[row++] = t;
-  if (tid == 1023) {
-    v.row_count[0] = s_part[1023];
-    if (count_out) count_out[0] = s_part[1023];
+    if (v.need[t]) {
+      if (v.tnet[t]) ++c1; else ++c0;
+    }
+  s_p0[tid] = c0;
+  s_p1[tid] = c1;
+  __syncthreads();
+  // inclusive Hillis-Steele scans over 1024 partials
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int a0 = tid >= off ? s_p0[tid - off] : 0;
+    const int a1 = tid >= off ? s_p1[tid - off] : 0;
+    __syncthreads();
+    s_p0[tid] += a0;
+    s_p1[tid] += a1;
+    __syncthreads();
   }
+  int r0 = s_p0[tid] - c0, r1 = v.seg1 + s_p1[tid] - c1;
+  for (int t = lo; t < hi; ++t)
+    if (v.need[t]) {
+      if (v.tnet[t]) v.row_tree[r1++] = t; else v.row_tree[r0++] = t;
+    }
+  if (tid == 1023) {
+    v.row_count[0] = s_p0[1023];
+    v.row_count[1] = s_p1[1023];
+    if (count_out) {
+      count_out[0] = s_p0[1023] + s_p1[1023];
+      count_out[1] = s_p0[1023];
+      count_out[2] = s_p1[1023];
+    }
+  }
+}
+
+__device__ __forceinline__ bool row_live(const View &v, int row) {
+  return row < v.seg1 ? row < v.row_count[0] : row - v.seg1 < v.row_count[1];
 }
 
 // ----------------------------------------------------------------------------
@@ -506,7 +534,7 @@ __global__ void k_encode(View v, void *out) {
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int row = (int)(gid / G::CELLS);
   const int cell = (int)(gid % G::CELLS);
-  if (row >= v.row_count[0]) return;
+  if (row >= v.T || !row_live(v, row)) return;
   const int t = v.row_tree[row];
   const int x = cell / G::H, y = cell % G::H;
   const uint64_t bit = 1ull << cell_bit<G>(x, y);
@@ -549,11 +577,16 @@ __global__ void k_encode(View v, void *out) {
 // kernel: expand + backup of network-evaluated leaves (mcts.py:316-321, :94-98)
 // ----------------------------------------------------------------------------
 template <class G>
-__global__ __launch_bounds__(64) void k_expand(View v, const float *probs, const float *values) {
+__global__ __launch_bounds__(64) void k_expand(View v, const float *probs0, const float *values0,
+                                               const float *probs1, const float *values1) {
   constexpr int P = G::APAD;
   const int lane = threadIdx.x & (P - 1);
   const int row = (blockIdx.x * blockDim.x + threadIdx.x) / P;
-  if (row >= v.row_count[0]) return;
+  if (row >= v.T || !row_live(v, row)) return;
+  // network-1 rows read their outputs from the second network's buffers (row - seg1)
+  const bool s1 = row >= v.seg1;
+  const float *prow = s1 ? probs1 + (size_t)(row - v.seg1) * G::A : probs0 + (size_t)row * G::A;
+  const float vrow = s1 ? values1[row - v.seg1] : values0[row];
   const int tree = v.row_tree[row];
   const size_t nb = nbase<G>(v, tree);
   const size_t bb = (size_t)tree * v.cap;
@@ -568,13 +601,13 @@ __global__ __launch_bounds__(64) void k_expand(View v, const float *probs, const
     const size_t ci = nb + (size_t)blk * P + lane;
     v.bn[ci] = 0;
     v.bw[ci] = 0.0;
-    v.bp[ci] = lane < G::A ? probs[(size_t)row * G::A + lane] : 0.f;
+    v.bp[ci] = lane < G::A ? prow[lane] : 0.f;
     v.bc[ci] = -1;
     v.bf64[ci] = 0;
   }
   const int mover = v.lmover[tree];
   // network(s, parent.player) returns value * player (modules.py:109-112)
-  const double val = (double)values[row] * (double)mover;
+  const double val = (double)vrow * (double)mover;
   const int plen = v.plen[tree];
   const size_t pb = (size_t)tree * G::MAXD;
   for (int k = lane; k < plen; k += P) {
@@ -766,8 +799,8 @@ __device__ void start_game(const View &v, int g, int64_t id, const float *priors
   v.mv_count[2 * g] = 0;
   v.mv_count[2 * g + 1] = 0;
   // policy.reset(-1 if swap else 1), opposing.reset(1 if swap else -1)  (:175-176)
-  reset_tree<G>(v, 2 * g, swap ? -1 : 1, priors ? priors : v.root_prior);
-  reset_tree<G>(v, 2 * g + 1, swap ? 1 : -1, priors ? priors + G::A : v.root_prior);
+  reset_tree<G>(v, 2 * g, swap ? -1 : 1, priors ? priors : v.root_prior + 16 * v.tnet[2 * g]);
+  reset_tree<G>(v, 2 * g + 1, swap ? 1 : -1, priors ? priors + G::A : v.root_prior + 16 * v.tnet[2 * g + 1]);
 }
 
 template <class G>
@@ -795,8 +828,53 @@ __global__ void k_games_begin_ply(View v) {
   // policy moves on even plies unless swap_sides (:178-183)
   const int mover = (v.gply[g] + v.gswap[g]) & 1;
   const int tree = 2 * g + mover;
+  if (v.tkind[tree] != SPMCTS_PLAYER_MCTS) {  // hard-coded players do not search
+    v.active[g] = -1;
+    return;
+  }
   v.active[g] = tree;
   draw_noise<G>(v, tree);
+}
+
+// Hard-coded opponents (games/general/hardcoded_players.py).  `own` = the player's stones,
+// `enemy` = the other side's, in the player's own env frame (its stones are +1: play_move passes
+// player * -1 to the opposing policy, selfplayworker.py:221-224); `look` = the player sign given to
+// reset(player) (selfplayworker.py:175-176), which OneStepLookahead uses as "self.player".
+// OneStepLookahead (:18-33): first any move after which step(a, look) ends the game, then any move
+// after which step(a, -look) does, else uniform over the legal moves.  Random (:45-49): uniform.
+// The uniform draw uses the tree's Philox stream (the reference's `random` module stream is not
+// reproduced).
+template <class G>
+__device__ int hardcoded_move(const View &v, int tree, int kind, Board envb, int look) {
+  const uint32_t legal = legal_mask<G>(envb);
+  if (kind == SPMCTS_PLAYER_LOOKAHEAD) {
+    for (int pass = 0; pass < 2; ++pass) {
+      const int who = pass == 0 ? look : -look;
+      for (int a = 0; a < G::A; ++a) {
+        if (!((legal >> a) & 1u)) continue;
+        Board b = envb;
+        int rew = 0, done = 0;
+        step<G>(b, a, who, &rew, &done);
+        if (done) return a;
+      }
+    }
+  }
+  const int n = popc((uint64_t)legal);
+  if (n == 0) return 0;
+  TreeRng r;
+  rng_load(v, tree, r);
+  bool terr = false;
+  const double u = rng_next(v, r, &terr);
+  rng_store(v, tree, r);
+  if (terr) set_err(v, SPMCTS_ERR_TAPE);
+  int k = (int)(u * (double)n);
+  if (k >= n) k = n - 1;
+  for (int a = 0; a < G::A; ++a)
+    if ((legal >> a) & 1u) {
+      if (k == 0) return a;
+      --k;
+    }
+  return 0;
 }
 
 template <class G>
@@ -808,8 +886,15 @@ __global__ void k_games_end_ply(View v) {
   const int tree = 2 * g + mover;
   const int m = v.mv_count[tree];
   float pr[G::A];
-  const PlayOut o = play_move_choice<G>(v, tree, 1.0, pr);
-  if (o.recorded) {
+  PlayOut o{0, false, 0.0, 0};
+  const int kind = v.tkind[tree];
+  if (kind == SPMCTS_PLAYER_MCTS) {
+    o = play_move_choice<G>(v, tree, 1.0, pr);
+  } else {
+    const Board envb = mover == 0 ? Board{v.gpos[g], v.gneg[g]} : Board{v.gneg[g], v.gpos[g]};
+    o.action = hardcoded_move<G>(v, tree, kind, envb, v.rplayer[tree]);
+  }
+  if (o.recorded && v.record) {
     if (m < G::MAXM) {
       const size_t rec = (size_t)tree * G::MAXM + m;
       write_state<G>(Board{v.rpos[tree], v.rneg[tree]}, v.mv_state + rec * G::CELLS);
@@ -835,8 +920,8 @@ __global__ void k_games_end_ply(View v) {
     v.gresult[g] = (int8_t)(rew * p_env);  // r = r * player (:218)
     return;  // both trees are discarded with the game
   }
-  set_node<G>(v, 2 * g, o.action);
-  set_node<G>(v, 2 * g + 1, o.action);
+  if (v.tkind[2 * g] == SPMCTS_PLAYER_MCTS) set_node<G>(v, 2 * g, o.action);
+  if (v.tkind[2 * g + 1] == SPMCTS_PLAYER_MCTS) set_node<G>(v, 2 * g + 1, o.action);
 }
 
 // finished games: offsets into the export ring + refill ids (single block, slot order)
@@ -1116,7 +1201,7 @@ static void plan_arena(spmcts_arena *h, Plan &pl) {
   pl.add(&v.active, std::max(T, G));
   pl.add(&v.row_tree, T);
   pl.add(&v.row_count, 4);
-  pl.add(&v.root_prior, 16);
+  pl.add(&v.root_prior, 32);  // [net][16]
   pl.add(&v.err, 4);
   pl.add(&v.gpos, G);
   pl.add(&v.gneg, G);
@@ -1141,6 +1226,9 @@ static void plan_arena(spmcts_arena *h, Plan &pl) {
   pl.add(&v.ex_count, 4);
   pl.add(&v.gcnt, 16);
   pl.add(&v.gscratch, 2 * G + 8);
+  pl.add(&v.tnet, T);
+  pl.add(&v.tkind, T);
+  pl.add(&v.budget, T);
 }
 
 static int setup_view(spmcts_arena *h, const spmcts_config *cfg) {
@@ -1168,6 +1256,9 @@ static int setup_view(spmcts_arena *h, const spmcts_config *cfg) {
   v.rng_mode = cfg->rng_mode;
   v.leaf_format = cfg->leaf_format;
   v.leaf_layout = cfg->leaf_layout;
+  v.seg1 = v.T;
+  v.record = 1;
+  v.sim = 0;
   if (v.T <= 0) return fail(-3, "n_trees must be > 0");
   if (v.G < 0 || 2 * (long long)v.G > v.T) return fail(-3, "games mode needs n_trees >= 2 * n_games");
   if (v.T > (1 << 24)) return fail(-3, "too many trees");
@@ -1186,6 +1277,9 @@ __global__ void k_rng_init(View v, uint64_t seed, uint64_t sub0) {
   ((int64_t *)v.tape_end)[t] = 0;
   v.need[t] = 0;
   v.noise_on[t] = 0;
+  v.tnet[t] = 0;
+  v.tkind[t] = SPMCTS_PLAYER_MCTS;
+  v.budget[t] = 0x7fffffff;
   for (int k = 0; k < C_NCNT; ++k) v.cnt[(size_t)t * C_NCNT + k] = 0;
 }
 
@@ -1197,6 +1291,7 @@ __global__ void k_games_init(View v) {
     v.ex_count[0] = 0;
     v.err[0] = 0;
     v.row_count[0] = 0;
+    v.row_count[1] = 0;
   }
   if (g >= v.G) return;
   v.gstate[g] = GS_IDLE;
@@ -1282,9 +1377,9 @@ int spmcts_arena_create(const spmcts_config *cfg, int device, spmcts_arena **out
   hipLaunchKernelGGL(k_rng_init, dim3(nblk(h->v.T, 256)), dim3(256), 0, 0, h->v, cfg->seed, cfg->subsequence0);
   hipLaunchKernelGGL(k_games_init, dim3(nblk(std::max(1, h->v.G), 256)), dim3(256), 0, 0, h->v);
   // default root prior: uniform (replaced by spmcts_set_root_prior)
-  std::vector<float> pri(16, 0.f);
-  for (int j = 0; j < h->A; ++j) pri[j] = 1.0f / h->A;
-  e = hipMemcpy(h->v.root_prior, pri.data(), 16 * sizeof(float), hipMemcpyHostToDevice);
+  std::vector<float> pri(32, 0.f);
+  for (int j = 0; j < h->A; ++j) pri[j] = pri[16 + j] = 1.0f / h->A;
+  e = hipMemcpy(h->v.root_prior, pri.data(), 32 * sizeof(float), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     for (void *q : h->allocs) (void)hipFree(q);
@@ -1346,6 +1441,7 @@ int spmcts_search_begin(spmcts_arena *h, const int32_t *trees_dev, int32_t n, sp
   if (!h) return fail(-1, "null arena");
   if (n > std::max(h->v.T, h->v.G)) return fail(-3, "too many active trees");
   h->n_active = n;
+  h->v.sim = 0;
   if (n <= 0) return 0;
   DISPATCH(h, hipLaunchKernelGGL(k_search_begin<GG>, dim3(nblk(n, 128)), dim3(128), 0, (hipStream_t)stream, h->v,
                                  trees_dev, n));
@@ -1371,6 +1467,7 @@ int spmcts_select_tree(spmcts_arena *h, spmcts_stream stream) {
     const int gpb = 64 / h->P;
     DISPATCH(h, hipLaunchKernelGGL(k_select<GG>, dim3(nblk(n, gpb)), dim3(64), 0, s, h->v, n));
   }
+  h->v.sim += 1;
   LAUNCH_CHECK();
   return 0;
 }
@@ -1386,12 +1483,66 @@ int spmcts_select(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_dev, sp
   return spmcts_leaf_rows(h, leaves_dev, leaf_count_dev, stream);
 }
 
-int spmcts_expand(spmcts_arena *h, const float *probs_dev, const float *values_dev, spmcts_stream stream) {
+int spmcts_expand2(spmcts_arena *h, const float *probs0_dev, const float *values0_dev, const float *probs1_dev,
+                   const float *values1_dev, spmcts_stream stream) {
   if (!h) return fail(-1, "null arena");
+  if (h->v.seg1 < h->v.T && (!probs1_dev || !values1_dev)) return fail(-1, "two-network arena needs network-1 outputs");
   const int gpb = 64 / h->P;
   DISPATCH(h, hipLaunchKernelGGL(k_expand<GG>, dim3(nblk(h->v.T, gpb)), dim3(64), 0, (hipStream_t)stream, h->v,
-                                 probs_dev, values_dev));
+                                 probs0_dev, values0_dev, probs1_dev, values1_dev));
   LAUNCH_CHECK();
+  return 0;
+}
+
+int spmcts_expand(spmcts_arena *h, const float *probs_dev, const float *values_dev, spmcts_stream stream) {
+  if (!h) return fail(-1, "null arena");
+  // one buffer indexed by row: network-1 rows (if any) sit at their own row index
+  const size_t s1 = (size_t)h->v.seg1;
+  const bool dual = h->v.seg1 < h->v.T;
+  return spmcts_expand2(h, probs_dev, values_dev, dual ? probs_dev + s1 * h->A : nullptr,
+                        dual ? values_dev + s1 : nullptr, stream);
+}
+
+int spmcts_set_tree_players(spmcts_arena *h, const uint8_t *nets, const uint8_t *kinds, const int32_t *budgets) {
+  if (!h) return fail(-1, "null arena");
+  const int T = h->v.T;
+  std::vector<uint8_t> nt(T, 0), kd(T, SPMCTS_PLAYER_MCTS);
+  std::vector<int32_t> bd(T, 0x7fffffff);
+  int n0 = 0;
+  for (int t = 0; t < T; ++t) {
+    if (nets) nt[t] = nets[t] ? 1 : 0;
+    if (kinds) {
+      if (kinds[t] > SPMCTS_PLAYER_LOOKAHEAD) return fail(-3, "unknown player kind");
+      kd[t] = kinds[t];
+    }
+    if (budgets) bd[t] = budgets[t] < 0 ? 0x7fffffff : budgets[t];
+    n0 += nt[t] ? 0 : 1;
+  }
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(h->v.tnet, nt.data(), T, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(h->v.tkind, kd.data(), T, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(h->v.budget, bd.data(), 4 * (size_t)T, hipMemcpyHostToDevice));
+  h->v.seg1 = n0;  // network-0 trees never have more than n0 pending leaves
+  return 0;
+}
+
+int spmcts_arena_segments(const spmcts_arena *h, int32_t *seg1) {
+  if (!h) return fail(-1, "null arena");
+  if (seg1) *seg1 = h->v.seg1;
+  return 0;
+}
+
+int spmcts_set_root_prior_net(spmcts_arena *h, int32_t net, const float *probs_dev, spmcts_stream stream) {
+  if (!h || !probs_dev) return fail(-1, "null argument");
+  if (net < 0 || net > 1) return fail(-3, "network index must be 0 or 1");
+  HIP_TRY(hipMemcpyAsync(h->v.root_prior + 16 * net, probs_dev, sizeof(float) * h->A, hipMemcpyDeviceToDevice,
+                         (hipStream_t)stream));
+  return 0;
+}
+
+int spmcts_games_set_record(spmcts_arena *h, int32_t record) {
+  if (!h) return fail(-1, "null arena");
+  h->v.record = record ? 1 : 0;
   return 0;
 }
 
@@ -1485,6 +1636,7 @@ int spmcts_games_begin_ply(spmcts_arena *h, spmcts_stream stream) {
   if (!h) return fail(-1, "null arena");
   if (h->v.G <= 0) return fail(-4, "arena has no game slots");
   h->n_active = h->v.G;
+  h->v.sim = 0;
   DISPATCH(h, hipLaunchKernelGGL(k_games_begin_ply<GG>, dim3(nblk(h->v.G, 128)), dim3(128), 0, (hipStream_t)stream,
                                  h->v));
   LAUNCH_CHECK();

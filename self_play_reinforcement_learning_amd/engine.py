@@ -18,12 +18,19 @@ with the next game id (swap_sides = id odd, self_play_parallel.py:237) until
 Network batches are padded up to a multiple of `bucket` rows (stale rows are
 evaluated and ignored), so the convolution library sees a handful of shapes
 instead of one per simulation.
+
+Evaluation games (SelfPlayWorker.set_up_policies(evaluate=True),
+selfplayworker.py:68-94; compare_models, self_play_parallel.py:355-379): pass
+`opponent=` a second network (its trees' leaves go to a second row segment
+evaluated by that network), or "random" / "lookahead" for the hard-coded
+players of games/general/hardcoded_players.py, optionally with its own
+`opponent_iterations`; `record=False` skips Move records (update=False).
 """
 import time
 
 import torch
 
-from . import distributed
+from . import _lib, distributed
 from .arena import Arena
 from .evaluator import make_evaluator
 
@@ -58,19 +65,43 @@ class EventTimer:
 class SelfPlayEngine:
     def __init__(self, game, network, n_games=4096, iterations=200, alpha=1.0, strong_play=False, evaluate=False,
                  seed=0, subsequence0=None, rng="philox", max_games=None, device=None, dtype=torch.bfloat16,
-                 leaf_layout="nhwc", cpuct=4.0, x_noise=0.25, blocks_per_tree=0, bucket=256):
+                 leaf_layout="nhwc", cpuct=4.0, x_noise=0.25, blocks_per_tree=0, bucket=256, opponent=None,
+                 opponent_iterations=None, record=True):
         self.game = game
-        self.iterations = iterations
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.evaluator = make_evaluator(network, game, device=self.device, dtype=dtype, leaf_layout=leaf_layout)
+        # the opposing player: self-play (same network), a second network, or a hard-coded player
+        self.evaluator1 = None
+        opp_kind = _lib.PLAYER_MCTS
+        if isinstance(opponent, str):
+            kinds = {"random": _lib.PLAYER_RANDOM, "lookahead": _lib.PLAYER_LOOKAHEAD,
+                     "onesteplookahead": _lib.PLAYER_LOOKAHEAD}
+            if opponent.lower() not in kinds:
+                raise ValueError(f"unknown hard-coded opponent {opponent!r} (random / lookahead)")
+            opp_kind = kinds[opponent.lower()]
+        elif opponent is not None and opponent is not network:
+            self.evaluator1 = make_evaluator(opponent, game, device=self.device, dtype=dtype, leaf_layout=leaf_layout)
+            e0, e1 = self.evaluator, self.evaluator1
+            if (e0.leaf_format, e0.leaf_layout) != (e1.leaf_format, e1.leaf_layout):
+                raise ValueError("both networks of an evaluation arena must take the same leaf format "
+                                 f"({e0.leaf_format}/{e0.leaf_layout} vs {e1.leaf_format}/{e1.leaf_layout})")
+        it1 = iterations if opponent_iterations is None else int(opponent_iterations)
+        self.iterations = max(iterations, it1) if opp_kind == _lib.PLAYER_MCTS else iterations
         rank = distributed.env_rank()[0]
         if subsequence0 is None:
             subsequence0 = rank * 2 * n_games  # disjoint Philox subsequences per rank
-        self.arena = Arena(game, n_trees=2 * n_games, n_games=n_games, iterations=iterations, rng=rng, seed=seed,
-                           subsequence0=subsequence0, strong_play=strong_play, evaluate=evaluate,
+        self.arena = Arena(game, n_trees=2 * n_games, n_games=n_games, iterations=self.iterations, rng=rng,
+                           seed=seed, subsequence0=subsequence0, strong_play=strong_play, evaluate=evaluate,
                            leaf_format=self.evaluator.leaf_format, leaf_layout=self.evaluator.leaf_layout,
                            cpuct=cpuct, x_noise=x_noise, alpha=alpha, blocks_per_tree=blocks_per_tree,
                            device=self.device)
+        if self.evaluator1 is not None or opp_kind != _lib.PLAYER_MCTS or it1 != iterations:
+            # tree 2g = the policy, 2g + 1 = the opposing player (selfplayworker.py:164-176)
+            self.arena.set_tree_players(nets=[0, 1 if self.evaluator1 is not None else 0] * n_games,
+                                        kinds=[_lib.PLAYER_MCTS, opp_kind] * n_games,
+                                        budgets=[iterations, it1] * n_games)
+        if not record:
+            self.arena.games_set_record(False)
         self.n_games = n_games
         self.max_games = max_games
         # torch convolutions want few distinct shapes; the fused HIP tower takes any batch
@@ -90,13 +121,17 @@ class SelfPlayEngine:
     def refresh_root_prior(self):
         """MCTreeSearch.reset evaluates the empty board (mcts.py:167-168); constant per weights."""
         a = self.arena
-        x = self.evaluator.empty_root_input(a.W, a.H, a.device)
-        probs, _ = self.evaluator(x)
-        a.set_root_prior(probs[0])
+        for net, ev in enumerate((self.evaluator, self.evaluator1)):
+            if ev is None:
+                continue
+            x = ev.empty_root_input(a.W, a.H, a.device)
+            probs, _ = ev(x)
+            a.set_root_prior(probs[0], net=net)
 
     def refresh_network(self):
-        if hasattr(self.evaluator, "refresh"):
-            self.evaluator.refresh()
+        for ev in (self.evaluator, self.evaluator1):
+            if ev is not None and hasattr(ev, "refresh"):
+                ev.refresh()
         self.refresh_root_prior()
 
     def enable_timers(self, on=True):
@@ -118,6 +153,8 @@ class SelfPlayEngine:
         if not n:
             return
         a = self.arena
+        if self.evaluator1 is not None:
+            return self._eval_expand2()
         m = min(a.max_rows, -(-n // self.bucket) * self.bucket)
         if self.nn_timer is not None:
             self.nn_timer.start()
@@ -128,15 +165,46 @@ class SelfPlayEngine:
         self.nn_rows += n
         self.nn_rows_padded += m
 
+    def _eval_expand2(self):
+        """Two networks: rows [0, n0) through the policy's, rows [seg1, seg1 + n1) through the opponent's."""
+        a = self.arena
+        n0, n1 = a.segment_counts()
+        outs = []
+        for ev, row0, n, cap in ((self.evaluator, 0, n0, a.seg1), (self.evaluator1, a.seg1, n1, a.max_rows - a.seg1)):
+            if n == 0:
+                outs.append((self._dummy_out(), torch.zeros(1, device=a.device)))
+                continue
+            m = min(cap, -(-n // self.bucket) * self.bucket)
+            if self.nn_timer is not None:
+                self.nn_timer.start()
+            outs.append(ev(a.leaves_from(row0, m)))
+            if self.nn_timer is not None:
+                self.nn_timer.stop()
+            self.nn_rows += n
+            self.nn_rows_padded += m
+        (p0, v0), (p1, v1) = outs
+        a.expand2(p0, v0, p1, v1)
+
+    def _dummy_out(self):
+        return torch.zeros((1, self.arena.A), dtype=torch.float32, device=self.arena.device)
+
     def _eval_expand_dev(self):
         """Network + expand on the device-side row count: no host synchronisation."""
         a = self.arena
         if self.nn_timer is not None:
             self.nn_timer.start()
-        probs, values = self.evaluator.forward_dev(a.leaves(a.max_rows), a.count_dev, a.max_rows)
+        if self.evaluator1 is None:
+            probs, values = self.evaluator.forward_dev(a.leaves(a.max_rows), a.count_dev, a.max_rows)
+        else:
+            probs, values = self.evaluator.forward_dev(a.leaves(a.seg1), a.segment_count_dev(0), a.seg1)
+            cap1 = a.max_rows - a.seg1
+            p1, v1 = self.evaluator1.forward_dev(a.leaves_from(a.seg1, cap1), a.segment_count_dev(1), cap1)
         if self.nn_timer is not None:
             self.nn_timer.stop()
-        a.expand(probs, values)
+        if self.evaluator1 is None:
+            a.expand(probs, values)
+        else:
+            a.expand2(probs, values, p1, v1)
 
     def ply(self, on_moves=None, refill=True):
         """Advance every active game by one move. Returns (#games finished, #records exported)."""
@@ -144,7 +212,7 @@ class SelfPlayEngine:
             self.start()
         a = self.arena
         a.games_begin_ply()
-        if getattr(self.evaluator, "supports_device_count", False) and self.async_device:
+        if self._device_count_ok():
             for _ in range(self.iterations):
                 a.select_async(self.select_timer)
                 self._eval_expand_dev()
@@ -165,6 +233,10 @@ class SelfPlayEngine:
         self.positions += exported
         self.plies += 1
         return finished, exported
+
+    def _device_count_ok(self):
+        return self.async_device and all(getattr(ev, "supports_device_count", False)
+                                         for ev in (self.evaluator, self.evaluator1) if ev is not None)
 
     def run(self, plies=None, games=None, seconds=None, on_moves=None):
         """Play until `plies` plies / `games` finished games / `seconds` elapse / the game budget is spent."""

@@ -229,11 +229,67 @@ class SelfPlayScheduler:
             reward = self.evaluate_policy(epoch)
             self.trainer.lr_step(reward)
 
+    # ------------------------------------------------------------------ evaluation games
+    def _opponent(self):
+        """The evaluation side of SelfPlayWorker.set_up_policies(evaluate=True) (selfplayworker.py:72-81):
+        (opponent for SelfPlayEngine, its iterations)."""
+        c = self.evaluation_policy_container
+        if c is None:
+            raise ValueError("evaluation games need an evaluation_policy_container")
+        gen = getattr(c, "policy_gen", None)
+        name = getattr(gen, "__name__", "").lower()
+        if name in ("random", "onesteplookahead"):
+            return ("random" if name == "random" else "lookahead"), None
+        kw = dict(getattr(c, "policy_kwargs", {}) or {})
+        net = self.evaluation_network
+        if net is None:
+            net = kw.get("network", kw.get("evaluator"))
+        if net is None:
+            raise ValueError("the evaluation MCTreeSearch has no network (pass evaluation_network=)")
+        pk = self._policy_kwargs()
+        for key, default in (("alpha", 1), ("strong_play", False)):
+            if kw.get(key, default) != pk.get(key, default):
+                logging.warning(f"evaluation policy {key}={kw.get(key, default)} differs from the policy's; "
+                                f"the arena uses the policy's value for both sides")
+        return net, kw.get("iterations", 100)
+
+    def _evaluation_engine(self, n_games):
+        opponent, opp_iters = self._opponent()
+        kw = self._policy_kwargs()
+        per_rank = max(1, n_games // self.world + (1 if self.rank < n_games % self.world else 0))
+        slots = min(per_rank, self.n_games or 4096)
+        self.network.eval()
+        return SelfPlayEngine(self.game, self.network, n_games=slots, iterations=kw.get("iterations", 100),
+                              alpha=kw.get("alpha", 1), strong_play=kw.get("strong_play", False), evaluate=True,
+                              seed=self.seed + 104729 + 7919 * self.rank, device=self.device, opponent=opponent,
+                              opponent_iterations=opp_iters, record=False), per_rank
+
+    def _play_evaluation(self, n_games):
+        """n_games evaluation games over all ranks (task i -> swap_sides = i odd, update=False);
+        returns the reference's result dicts (self_play_parallel.py:294-300, :366-371)."""
+        if n_games <= 0:
+            return []
+        eng, per_rank = self._evaluation_engine(n_games)
+        c0 = eng.counters()["results"]
+        eng.play_games(per_rank)
+        eng.check()
+        c1 = eng.counters()["results"]
+        flat = [c1[s][k] - c0[s][k] for s in range(2) for k in range(3)]
+        flat = [int(x) for x in D.all_reduce_stats(flat)]
+        reward_list = []
+        for s in range(2):
+            for k, r in enumerate((1, 0, -1)):
+                reward_list += [{"reward": r, "swap_sides": bool(s)}] * flat[3 * s + k]
+        eng.arena.close()
+        return reward_list
+
     def run_evaluation_games(self):
-        """self_play_parallel.py:294-300 — needs a two-network arena."""
-        if self.evaluation_policy_container is None:
+        """self_play_parallel.py:294-300: evaluation_games games of the policy against the
+        evaluation policy (both in evaluate mode, no Move records); results -> result_queue."""
+        if self.evaluation_policy_container is None or not self.evaluation_games:
             return
-        logging.info("evaluation games against a separate policy are not implemented on the arena yet")
+        for r in self._play_evaluation(self.evaluation_games):
+            self.result_queue.put(r)
 
     def parse_results(self, reward_list):
         """self_play_parallel.py:302-327"""
@@ -255,18 +311,30 @@ class SelfPlayScheduler:
         return total_rewards, breakdown
 
     def evaluate_policy(self, epoch):
+        """self_play_parallel.py:329-353: parse the self-play results, then play and parse evaluation games."""
         reward_list = []
         while not self.result_queue.empty():
             reward_list.append(self.result_queue.get())
         total = 0
         if epoch >= 0 and reward_list:
             total, _ = self.parse_results(reward_list)
+        if self.evaluation_policy_container is None or not self.evaluation_games:
+            return total
         self.run_evaluation_games()
+        reward_list = []
+        while not self.result_queue.empty():
+            reward_list.append(self.result_queue.get())
+        total, _ = self.parse_results(reward_list)
         return total
 
     def compare_models(self, num_workers=None, inference_proxy=True, threads_per_worker=8, resume_model=False):
-        """self_play_parallel.py:355-379 with both sides MCTreeSearch on the arena (policy vs evaluation net)."""
-        raise NotImplementedError("two-network arena evaluation is the next milestone (SURVEY §8(f) rank 3)")
+        """self_play_parallel.py:355-379: epoch_length evaluation games, policy network vs the
+        evaluation policy (a second network on the same arena, or a hard-coded player).
+        Returns (total_rewards, breakdown) exactly as the reference's parse_results."""
+        if resume_model:
+            self._load_latest(prev_run=True)
+        reward_list = self._play_evaluation(self.epoch_length)
+        return self.parse_results(reward_list)
 
 
 class _Trainer:
@@ -307,7 +375,7 @@ class _Trainer:
         loss.backward()
         self.optim.step()
         self.network.eval()
-        return float(loss)
+        return float(loss.detach())
 
     def lr_step(self, reward):
         self.scheduler.step(reward)

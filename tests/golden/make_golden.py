@@ -23,6 +23,14 @@ Fixtures
      the memory queue (mcts.py:225-232) and evaluate-mode games.
   G4 net_io.npz  ResidualTower (games/general/modules.py:43-125) forward outputs
      for seeded random-init nets, pinning the build's own net definition.
+  G5 arena_games.json  evaluation games (SelfPlayWorker.set_up_policies(evaluate=True),
+     selfplayworker.py:68-94; play_episode(update=False)): the policy MCTreeSearch
+     against a second MCTreeSearch with its own table net and its own iteration
+     count, or against the hard-coded OneStepLookahead / Random players
+     (games/general/hardcoded_players.py), whose `random.choice` draws are logged
+     as (n, index).
+
+    python tests/golden/make_golden.py G5     # regenerate one fixture only
 """
 import json
 import os
@@ -54,6 +62,91 @@ def _ref_imports():
     from games.tictactoe.tictactoe_env import TicTacToeEnv
 
     return ref_mcts, SelfPlayer, Connect4Env, TicTacToeEnv, GameOver, ResidualTower
+
+
+# ----------------------------------------------------------------------------- G5
+class _ChoiceSpy:
+    """Stands in for the `random` module inside hardcoded_players: forwards to the real
+    global `random.choice` and logs (len(seq), index of the result)."""
+
+    def __init__(self, log):
+        self.log = log
+
+    def choice(self, seq):
+        x = random.choice(seq)
+        self.log.append((len(seq), list(seq).index(x)))
+        return x
+
+
+def gen_arena_games(ref_mcts, SelfPlayer, Connect4Env, TicTacToeEnv):
+    from games.general import hardcoded_players as hp
+
+    MCTreeSearch = ref_mcts.MCTreeSearch
+    orig_play = MCTreeSearch._play
+    orig_random = hp.random
+    log, choices = [], []
+
+    def spy_play(self, temp=0.05):
+        root = self.root_node
+        pre = dict(tree=getattr(self, "_golden_tree", -1), child_n=[int(c.n) for c in root.children],
+                   child_w=[float(c.w) for c in root.children], root_n=int(root.n), root_w=float(root.w))
+        a = orig_play(self, temp)
+        pre["action"] = int(a)
+        log.append(pre)
+        return a
+
+    MCTreeSearch._play = spy_play
+    hp.random = _ChoiceSpy(choices)
+    plan = [  # game, EnvCls, A, policy sims, opponent kind, opponent sims, count
+        ("connect4", Connect4Env, 7, 25, "mcts", 40, 8),
+        ("tictactoe", TicTacToeEnv, 9, 25, "mcts", 10, 8),
+        ("connect4", Connect4Env, 7, 25, "lookahead", 0, 8),
+        ("connect4", Connect4Env, 7, 25, "random", 0, 6),
+        ("tictactoe", TicTacToeEnv, 9, 25, "lookahead", 0, 8),
+        ("tictactoe", TicTacToeEnv, 9, 25, "random", 0, 6),
+    ]
+    games = []
+    gid = 0
+    try:
+        for game, EnvCls, A, sims, kind, opp_sims, count in plan:
+            for k in range(count):
+                seed = 50_000 + gid
+                swap = bool(k % 2)
+                salt_p, salt_o = 5 * gid + 1, 5 * gid + 2
+                np.random.seed(seed)
+                random.seed(seed)
+                rq = _ListQueue()
+                pol = MCTreeSearch(network=TableNet(A, salt=salt_p), env=EnvCls, memory_queue=None, iterations=sims)
+                pol.train(False)
+                if kind == "mcts":
+                    opp = MCTreeSearch(network=TableNet(A, salt=salt_o), env=EnvCls, memory_queue=None,
+                                       iterations=opp_sims)
+                    opp._golden_tree = 1
+                elif kind == "lookahead":
+                    opp = hp.OneStepLookahead(env=EnvCls)
+                else:
+                    opp = hp.Random(env=EnvCls)
+                opp.env = EnvCls()
+                opp.train(False)
+                pol.evaluate(True)  # set_up_policies(evaluate=True): both sides try their hardest
+                opp.evaluate(True)
+                pol._golden_tree = 0
+                sp = SelfPlayer(pol, opp, EnvCls(), rq)
+                del log[:]
+                del choices[:]
+                states, r = sp.play_episode(swap_sides=swap, update=False)
+                games.append(dict(
+                    id=gid, game=game, sims=sims, opponent=kind, opponent_sims=opp_sims, seed=seed,
+                    swap_sides=swap, salt_policy=salt_p, salt_opponent=salt_o, result=int(r),
+                    results_queue=[dict(reward=int(x["reward"]), swap_sides=bool(x["swap_sides"])) for x in rq.items],
+                    plies=[dict(x) for x in log], choices=[list(c) for c in choices],
+                    final_board=np.asarray(states[-1]).astype(int).reshape(-1).tolist(),
+                ))
+                gid += 1
+    finally:
+        MCTreeSearch._play = orig_play
+        hp.random = orig_random
+    return games
 
 
 # ----------------------------------------------------------------------------- G1
@@ -399,6 +492,12 @@ def gen_net_io(ResidualTower, Connect4Env, TicTacToeEnv):
 def main():
     ref_mcts, SelfPlayer, Connect4Env, TicTacToeEnv, GameOver, ResidualTower = _ref_imports()
     torch.set_num_threads(4)
+    only = sys.argv[1:]
+    if only == ["G5"]:
+        print("G5 arena games ...", flush=True)
+        with open(os.path.join(HERE, "arena_games.json"), "w") as f:
+            json.dump(gen_arena_games(ref_mcts, SelfPlayer, Connect4Env, TicTacToeEnv), f)
+        return
     print("G1 env KATs ...", flush=True)
     np.savez_compressed(os.path.join(HERE, "env_kat_c4.npz"), **gen_env_kat_c4(Connect4Env, GameOver))
     np.savez_compressed(os.path.join(HERE, "env_kat_ttt.npz"), **gen_env_kat_ttt(TicTacToeEnv, GameOver))
@@ -412,6 +511,9 @@ def main():
         json.dump(games, f)
     print("G4 net I/O ...", flush=True)
     np.savez_compressed(os.path.join(HERE, "net_io.npz"), **gen_net_io(ResidualTower, Connect4Env, TicTacToeEnv))
+    print("G5 arena games ...", flush=True)
+    with open(os.path.join(HERE, "arena_games.json"), "w") as f:
+        json.dump(gen_arena_games(ref_mcts, SelfPlayer, Connect4Env, TicTacToeEnv), f)
     print("done")
 
 

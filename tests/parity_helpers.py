@@ -58,6 +58,22 @@ def g3_tapes(g):
     return rec_p.tape, rec_o.tape, (r, moves, log)
 
 
+def g5_tapes(g):
+    """Per-tree tapes of one G5 evaluation game (policy tree, opposing player)."""
+    from oracle.hardcoded import PyRandomRNG
+
+    A = A_OF[g["game"]]
+    net_p, net_o = TableNet(A, g["salt_policy"]), TableNet(A, g["salt_opponent"])
+    np.random.seed(g["seed"])
+    base = NumpyRNG()
+    rec_p = RecordingRNG(base)
+    rec_o = RecordingRNG(base if g["opponent"] == "mcts" else PyRandomRNG(g["seed"]))
+    # update=True only adds the end-of-game push (no RNG draws): the Moves the arena records
+    out = play_episode(g["game"], net_p, net_o, rec_p, rec_o, g["sims"], swap_sides=g["swap_sides"], update=True,
+                       evaluate=True, opponent=g["opponent"], opponent_iterations=g["opponent_sims"] or None)
+    return rec_p.tape, rec_o.tape, out
+
+
 def group_by(items, keys):
     out = {}
     for it in items:
@@ -165,3 +181,78 @@ def run_g3_group(games, leaf_format="f32", leaf_layout="nchw"):
     arena.close()
     merged = {k: np.concatenate([r[k].numpy() for r in records]) for k in records[0]} if records else None
     return merged, counters
+
+
+def run_g5_group(games, record=True):
+    """Run a group of G5 evaluation games (same game / sims / opponent) as game slots of one
+    two-player arena: network-1 rows for a second table net, or hard-coded opponents (tape mode)."""
+    import torch
+
+    from self_play_reinforcement_learning_amd import _lib
+    from self_play_reinforcement_learning_amd.arena import Arena
+    from self_play_reinforcement_learning_amd.arena import table_net_eval
+
+    g0 = games[0]
+    game, sims, opp, opp_sims = g0["game"], g0["sims"], g0["opponent"], g0["opponent_sims"]
+    G = len(games)
+    kind = {"mcts": _lib.PLAYER_MCTS, "lookahead": _lib.PLAYER_LOOKAHEAD, "random": _lib.PLAYER_RANDOM}[opp]
+    arena = Arena(game, n_trees=2 * G, n_games=G, iterations=max(sims, opp_sims), rng="tape", evaluate=True)
+    arena.set_tree_players(nets=[0, 1 if opp == "mcts" else 0] * G, kinds=[_lib.PLAYER_MCTS, kind] * G,
+                           budgets=[sims, opp_sims if opp == "mcts" else 0] * G)
+    arena.games_set_record(record)
+    tapes, oracle = [], []
+    for g in games:
+        tp, to, out = g5_tapes(g)
+        tapes += [tp, to]
+        oracle.append(out)
+    arena.set_tapes(tapes)
+    salts = []
+    for g in games:
+        salts += [g["salt_policy"], g["salt_opponent"]]
+    salts_by_tree = torch.tensor(salts, dtype=torch.int64, device=arena.device)
+    priors = np.stack([np.stack([empty_prior(game, g["salt_policy"]), empty_prior(game, g["salt_opponent"])])
+                       for g in games])
+    arena.games_set_limit(G)
+    arena.games_start(list(range(G)), priors=priors)
+    records, rows = [], [0, 0]
+
+    def seg_eval(row0, n, trees_all):
+        if n == 0:
+            z = torch.zeros((1, arena.A), device=arena.device)
+            return z, torch.zeros(1, device=arena.device)
+        trees = trees_all[row0:row0 + n].long()
+        return table_net_eval(game, arena.leaves_from(row0, n), arena.leaf_format, arena.leaf_layout,
+                              salts=salts_by_tree[trees].contiguous())
+
+    def step(count):
+        if not count:
+            return
+        n0, n1 = arena.segment_counts()
+        assert n0 + n1 == count
+        rows[0] += n0
+        rows[1] += n1
+        trees_all = arena.leaf_trees(arena.n_trees)
+        p0, v0 = seg_eval(0, n0, trees_all)
+        p1, v1 = seg_eval(arena.seg1, n1, trees_all)
+        arena.expand2(p0, v0, p1, v1)
+
+    plies = np.zeros(G, dtype=int)
+    for _ in range(64):
+        st = arena.games_state()
+        plies = np.where(st["state"] == 1, st["ply"], plies)
+        arena.games_begin_ply()
+        for _ in range(max(sims, opp_sims)):
+            step(arena.select())
+        step(arena.games_end_ply())
+        fin, ring = arena.games_finish_ply(refill=False)
+        if ring:
+            records.append({k: v.cpu() for k, v in arena.export_moves(ring).items()})
+        st = arena.games_state()
+        plies = np.where(st["ply"] > plies, st["ply"], plies)
+        if not (st["state"] == 1).any():
+            break
+    arena.check()
+    counters = arena.counters()
+    arena.close()
+    merged = {k: np.concatenate([r[k].numpy() for r in records]) for k in records[0]} if records else None
+    return merged, counters, oracle, rows

@@ -138,3 +138,91 @@ def test_scheduler_train_model_dropin(tmp_path):
     assert sp.engine.games_done == 16 + 2 * 24
     m = sp.trainer.memory.sample(4)
     assert m[0].state.shape == (7, 6) and m[0].tree_probs.shape == (7,) and m[0].actual_val.dtype == torch.float32
+
+
+def _tower(seed, blocks=2, ff=32):
+    torch.manual_seed(seed)
+    return ResidualTowerCls()(7, 6, 7, num_blocks=blocks, filter_factor=ff).cuda().eval()
+
+
+def ResidualTowerCls():
+    from self_play_reinforcement_learning_amd.modules import ResidualTower
+
+    return ResidualTower
+
+
+def _run_engine(**kw):
+    from self_play_reinforcement_learning_amd.engine import SelfPlayEngine
+
+    async_device = kw.pop("async_device", True)
+    eng = SelfPlayEngine("connect4", **kw)
+    eng.async_device = async_device
+    got = []
+    eng.run(games=kw["max_games"], on_moves=lambda m: got.append({k: v.cpu().numpy() for k, v in m.items()}))
+    eng.check()
+    moves = {k: np.concatenate([g[k] for g in got]) for k in got[0]} if got else None
+    return eng, moves, eng.counters()
+
+
+@pytest.mark.parametrize("opp_iters", [12, 20])
+def test_two_network_arena_async_matches_sync(opp_iters):
+    """Evaluation games between two fused-tower networks (row segments per network, per-player
+    iteration budgets): the device-count loop equals the host-synchronised loop exactly."""
+    a, b = _tower(0), _tower(1)
+    out = []
+    for async_device in (True, False):
+        eng, moves, c = _run_engine(network=a, opponent=b, opponent_iterations=opp_iters, n_games=40, iterations=12,
+                                    seed=5, max_games=40, evaluate=True, async_device=async_device)
+        assert eng.evaluator1 is not None and eng.arena.seg1 == 40
+        out.append((moves, c))
+    (m1, c1), (m2, c2) = out
+    for k in m1:
+        np.testing.assert_array_equal(m1[k], m2[k], err_msg=k)
+    for k in ("sims", "moves", "nn_leaves", "terminal_leaves", "depth_sum", "games_finished", "results"):
+        assert c1[k] == c2[k], k
+    assert c1["games_finished"] == 40
+
+
+def test_two_network_arena_uses_each_network():
+    """Swapping in the same network as the opponent gives the self-play results; a different
+    opponent network changes them."""
+    a, b = _tower(0), _tower(1)
+    _, m_self, c_self = _run_engine(network=a, n_games=32, iterations=10, seed=9, max_games=32)
+    _, m_same, c_same = _run_engine(network=a, opponent=_tower(0), n_games=32, iterations=10, seed=9, max_games=32)
+    _, m_diff, _ = _run_engine(network=a, opponent=b, n_games=32, iterations=10, seed=9, max_games=32)
+    for k in m_self:
+        np.testing.assert_array_equal(m_self[k], m_same[k], err_msg=k)
+    assert c_self["results"] == c_same["results"]
+    assert m_self["z"].shape != m_diff["z"].shape or not np.array_equal(m_self["tree_probs"], m_diff["tree_probs"])
+
+
+@pytest.mark.parametrize("opponent", ["random", "lookahead"])
+def test_hardcoded_opponents_on_device(opponent):
+    a = _tower(0)
+    eng, moves, c = _run_engine(network=a, opponent=opponent, n_games=64, iterations=8, seed=2, max_games=64,
+                                evaluate=True)
+    assert c["games_finished"] == 64 and c["error_flags"] == 0
+    assert np.array(c["results"]).sum() == 64
+    # only the policy's moves are recorded; the policy's tree searched every one of its plies
+    assert c["moves"] == moves["z"].shape[0] == c["positions_exported"]
+    for gid in np.unique(moves["game"]):
+        assert len(np.unique(moves["z"][moves["game"] == gid])) == 1
+
+
+def test_compare_models_dropin(tmp_path):
+    """compare_models (self_play_parallel.py:355-379) with a second MCTreeSearch network and with a
+    hard-coded evaluation player: (total_rewards, breakdown) over epoch_length games."""
+    from self_play_reinforcement_learning_amd import (Connect4Env, MCTreeSearch, ModelContainer, OneStepLookahead,
+                                                      SelfPlayScheduler)
+
+    a, b = _tower(0), _tower(1)
+    for ev in (ModelContainer(policy_gen=MCTreeSearch, policy_kwargs=dict(iterations=6, env=Connect4Env)),
+               ModelContainer(policy_gen=OneStepLookahead, policy_kwargs=dict(env=Connect4Env))):
+        container = ModelContainer(policy_gen=MCTreeSearch, policy_kwargs=dict(iterations=8, env=Connect4Env))
+        sp = SelfPlayScheduler(policy_container=container, env=Connect4Env, network=a, evaluation_policy_container=ev,
+                               evaluation_network=b, epoch_length=30, save_dir=str(tmp_path), n_games=16)
+        total, breakdown = sp.compare_models()
+        n = sum(v for side in breakdown.values() for v in side.values())
+        assert n == 30
+        assert total == sum(s["wins"] - s["losses"] for s in breakdown.values())
+        assert sum(breakdown["first"].values()) == 15 and sum(breakdown["second"].values()) == 15

@@ -70,3 +70,41 @@ def test_tower_rows_independent_of_batch():
     # offset windows: a board's result does not depend on its neighbours in the tile
     p, v = hip(x[3:40])
     assert torch.equal(p, full_p[3:40]) and torch.equal(v, full_v[3:40])
+
+
+@pytest.mark.parametrize("n", [1, 37, 700, 1536])
+def test_forward_dev_matches_host_count(n):
+    """The device-count launch (row count read on device, full/half workgroups chosen on device)
+    gives the host-count results bit for bit on the live rows."""
+    W, H, A = 7, 6, 7
+    net = _net(W, H, A, 2, 32)
+    max_rows = 2048
+    x = _planes(W, H, max_rows, seed=5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    hip = HipTowerEvaluator(net)
+    p, v = hip(x[:n].contiguous(memory_format=torch.channels_last))
+    cnt = torch.tensor([n], dtype=torch.int32, device=x.device)
+    pd, vd = hip.forward_dev(x, cnt, max_rows)
+    torch.cuda.synchronize()
+    assert torch.equal(pd[:n], p) and torch.equal(vd[:n].view(-1), v.view(-1))
+
+
+def test_engine_async_matches_sync_path():
+    """A ply loop driven by the device-side leaf count reproduces the host-synchronised loop exactly."""
+    from self_play_reinforcement_learning_amd.engine import SelfPlayEngine
+
+    net = _net(7, 6, 7, 2, 32)
+    out = []
+    for async_device in (True, False):
+        eng = SelfPlayEngine("connect4", net, n_games=48, iterations=12, seed=7, max_games=48)
+        assert eng.evaluator.supports_device_count
+        eng.async_device = async_device
+        got = []
+        eng.run(games=48, on_moves=lambda m: got.append({k: v.cpu().numpy() for k, v in m.items()}))
+        eng.check()
+        c = eng.counters()
+        out.append(({k: np.concatenate([g[k] for g in got]) for k in got[0]}, c))
+    (m1, c1), (m2, c2) = out
+    for k in m1:
+        np.testing.assert_array_equal(m1[k], m2[k], err_msg=k)
+    for k in ("sims", "moves", "nn_leaves", "terminal_leaves", "depth_sum", "games_finished"):
+        assert c1[k] == c2[k], k

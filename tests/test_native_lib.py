@@ -68,3 +68,42 @@ def test_env_facade_plays_a_game():
     assert r == 1 and d and heights[0] == 4
     with pytest.raises(GameOver):
         e.step(2, -1)
+
+
+@pytest.mark.parametrize("game", ["connect4", "tictactoe"])
+def test_host_hardcoded_players_match_oracle(game):
+    """OneStepLookahead / Random (host API twins of the device players) vs the oracle restatement."""
+    import random
+
+    from oracle.envs import make_env
+    from oracle.hardcoded import HardcodedPlayer, PyRandomRNG
+    from self_play_reinforcement_learning_amd.envs import Connect4Env, TicTacToeEnv
+    from self_play_reinforcement_learning_amd.hardcoded_players import OneStepLookahead, Random
+
+    Env = Connect4Env if game == "connect4" else TicTacToeEnv
+    rng = np.random.default_rng(3)
+    for case in range(150):
+        ref = make_env(game)
+        ref.reset()
+        plays, player = [], 1
+        for _ in range(int(rng.integers(0, 12 if game == "connect4" else 6))):
+            legal = np.flatnonzero(ref.valid_moves())
+            a = int(rng.choice(legal))
+            _, _, done, _ = ref.step(a, player)
+            if done:
+                break
+            plays.append((a, player))
+            player = -player
+        if ref.episode_over if hasattr(ref, "episode_over") else False:
+            continue
+        for kind, Cls in (("lookahead", OneStepLookahead), ("random", Random)):
+            look = 1 if case % 2 else -1
+            host = Cls(env=Env)
+            host.reset(look)
+            orc = HardcodedPlayer(kind, game, PyRandomRNG(case))
+            orc.reset(look)
+            for a, p in plays:
+                host.play_action(a, p)
+                orc.play_action(a, p)
+            random.seed(case)
+            assert host(None) == orc.move(), (case, kind, plays)

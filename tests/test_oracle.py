@@ -117,3 +117,49 @@ def test_selfplay_games_match_reference(idx):
         assert float(m["actual_val"]) == M["actual_val"]
         assert m["tree_probs"].astype(float).tolist() == M["tree_probs"]
         assert float(m["q"]) == M["q"]
+
+
+def _g5_run(g, rng_p=None, rng_o=None):
+    from oracle.hardcoded import PyRandomRNG
+
+    A = A_OF[g["game"]]
+    net_p = TableNet(A, g["salt_policy"])
+    net_o = TableNet(A, g["salt_opponent"])
+    np.random.seed(g["seed"])
+    rng = NumpyRNG()
+    if g["opponent"] != "mcts":
+        rng_o = rng_o or PyRandomRNG(g["seed"])  # random.seed(seed) in the generator
+    return play_episode(g["game"], net_p, net_o, rng_p or rng, rng_o or rng, g["sims"],
+                        swap_sides=g["swap_sides"], update=False, evaluate=True, opponent=g["opponent"],
+                        opponent_iterations=g["opponent_sims"] or None)
+
+
+@pytest.mark.parametrize("idx", range(44))
+def test_evaluation_games_match_reference(idx):
+    """G5: policy vs a second network with its own iteration count, or vs OneStepLookahead / Random."""
+    g = load_json("arena_games.json")[idx]
+    r, moves, log, (pol, opp, env) = _g5_run(g)
+    assert r == g["result"] and moves == []
+    assert g["results_queue"] == [dict(reward=r, swap_sides=g["swap_sides"])]
+    searched = [L for L in log if "child_n" in L]
+    assert len(searched) == len(g["plies"])
+    for L, P in zip(searched, g["plies"]):
+        for k in ("tree", "action", "child_n", "child_w", "root_n", "root_w"):
+            assert L[k] == P[k], k
+    assert env.board.reshape(-1).astype(int).tolist() == g["final_board"]
+    if g["opponent"] != "mcts":  # the hard-coded player's random.choice draws, in order
+        from oracle.hardcoded import PyRandomRNG
+
+        class Log(PyRandomRNG):
+            def __init__(self, seed):
+                super().__init__(seed)
+                self.log = []
+
+            def choice_index(self, n):
+                k = super().choice_index(n)
+                self.log.append([n, k])
+                return k
+
+        lg = Log(g["seed"])
+        _g5_run(g, rng_o=lg)
+        assert lg.log == g["choices"]
