@@ -16,6 +16,7 @@ ap.add_argument("--batch", type=int, default=4096)
 ap.add_argument("--ff", type=int, default=32)
 ap.add_argument("--blocks", type=int, default=20)
 ap.add_argument("--iters", type=int, default=20)
+ap.add_argument("--trunk-only", action="store_true")
 args = ap.parse_args()
 torch.manual_seed(0)
 net = ResidualTower(7, 6, 7, num_blocks=args.blocks, filter_factor=args.ff).cuda().eval()
@@ -23,6 +24,22 @@ b = torch.randint(-1, 2, (args.batch, 7, 6))
 x = planes_from_boards(b, 7, 6).cuda().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
 fl = resnet_flops_per_leaf(7, 6, 7, args.ff, args.blocks) * args.batch
 out = {}
+if args.trunk_only:
+    ev = HipTowerEvaluator(net)
+    xt = x.permute(0, 2, 3, 1)
+    for _ in range(3):
+        ev.trunk(xt)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(args.iters):
+        ev.trunk(xt)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / args.iters
+    print(json.dumps(dict(batch=args.batch, cg=os.environ.get("SPMCTS_TOWER_CG"), trunk_ms=ms,
+                          tflops=fl / ms / 1e9)))
+    sys.exit(0)
 for name, ev in (("hip", HipTowerEvaluator(net)), ("hip_fusedheads", HipTowerEvaluator(net, fused_heads=True)),
                  ("hip_torchheads", HipTowerEvaluator(net, fused_heads=False)),
                  ("torch_bf16", TowerEvaluator(net, dtype=torch.bfloat16))):

@@ -30,11 +30,22 @@ namespace tower {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
 
 
-template <int C_, int ROWS_, int W_, int H_, int CG_ = 2, int WAVES_ = 4>
+template <int C_, int ROWS_, int W_, int H_, int CG_ = 2, int WAVES_ = 4, int ABL_ = 0, int DEPTH_ = 4>
 struct Cfg {
+  static constexpr int DEPTH = DEPTH_;  // weight-fragment prefetch distance (k-steps)
   static constexpr int C = C_, ROWS = ROWS_, W = W_, H = H_;
+  // ABL: timing ablations for kernel analysis only (results are wrong): 1 = no accumulator init,
+  // 2 = no epilogue store, 4 = no inter-layer barrier, 8 = no LDS operand reads in the k-loop,
+  // 16 = no weight loads in the k-loop, 128 = half the weight loads (m = 0 only).
+  // Schedule/epilogue alternatives (correct results): 64 = accumulator init with bias/residual
+  // (instead of a zero first k-step and bias/residual in the epilogue), 256 = loads issued in a
+  // burst between MFMA blocks (instead of one per MFMA gap), 2048 = packed-math epilogue.
+  static constexpr int ABL = ABL_;
   static constexpr int WAVES = WAVES_, THREADS = 64 * WAVES_;
   static constexpr int CG = CG_;            // waves split output channels into CG groups ...
   static constexpr int MG = WAVES_ / CG_;   // ... and cell rows into MG groups
@@ -43,9 +54,12 @@ struct Cfg {
   static constexpr int VROWS = BOARDS * CELLS;
   static constexpr int RS = C * 2 + 16;  // bytes per LDS row
   static constexpr int ZROW = ROWS;
+  // 16 zero rows: an off-board neighbour reads the zero row in its own bank position (rows r and
+  // r + 16 share banks at a 4-dword row shift), so zero reads never conflict with on-board reads
+  static constexpr int NZ = 16;
   static constexpr int NT = ROWS / 32 / MG;  // 32-cell tiles per wave
   static constexpr int MT = C / 32 / CG;     // 32-channel tiles per wave
-  static constexpr int BUF = (ROWS + 1) * RS;
+  static constexpr int BUF = (ROWS + NZ) * RS;
   static constexpr int LDS = 2 * BUF;
   static constexpr int HEAD = C / 2;  // policy filter_factor | value filter_factor channels (filter_factor = C/4)
   static constexpr int HCT = HEAD / 32;  // head channel tiles
@@ -67,12 +81,14 @@ __device__ __forceinline__ bf16x8 lds_b128(const char *p) { return *(const bf16x
 template <class K>
 struct Nbr {
   int base[K::NT];
+  int rowi[K::NT];
   uint32_t mask[K::NT];
   __device__ __forceinline__ void init(int r, int mg) {
 #pragma unroll
     for (int t = 0; t < K::NT; ++t) {
       const int row = (mg * K::NT + t) * 32 + r;
       base[t] = row * K::RS;
+      rowi[t] = row;
       uint32_t m = 0;
       if (row < K::VROWS) {
         const int c = row % K::CELLS, x = c / K::H, y = c % K::H;
@@ -88,7 +104,8 @@ struct Nbr {
   // byte offset of the source row of tile t for `tap` (the zero row when off the board)
   __device__ __forceinline__ int off(int t, int tap) const {
     const int d = ((tap / 3 - 1) * K::H + (tap % 3 - 1)) * K::RS;
-    return ((mask[t] >> tap) & 1u) ? base[t] + d : K::ZROW * K::RS;
+    const int dr = (tap / 3 - 1) * K::H + (tap % 3 - 1);
+    return ((mask[t] >> tap) & 1u) ? base[t] + d : (K::ZROW + ((rowi[t] + dr) & (K::NZ - 1))) * K::RS;
   }
 };
 
@@ -118,6 +135,75 @@ __device__ __forceinline__ void acc_init(f32x16 (&acc)[K::MT][K::NT], const char
         acc[m][t][4 * g + 1] = v1;
         acc[m][t][4 * g + 2] = v2;
         acc[m][t][4 * g + 3] = v3;
+      }
+    }
+}
+
+// Epilogue with bias (and residual) added here instead of in the accumulator init (the first
+// k-step's MFMAs then start from zero): out = relu(acc + bias (+ dst)), bf16, into dst.
+template <class K, bool RESID>
+__device__ __forceinline__ void acc_store_bias_relu(const f32x16 (&acc)[K::MT][K::NT], char *dst, const float *bias,
+                                                    int wave, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int m = 0; m < K::MT; ++m)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int ch = ((wave % K::CG) * K::MT + m) * 32 + 8 * g + 4 * h;
+      const float4 bv = *(const float4 *)(bias + ch);
+#pragma unroll
+      for (int t = 0; t < K::NT; ++t) {
+        char *p = dst + (((wave / K::CG) * K::NT + t) * 32 + r) * K::RS + ch * 2;
+        float v0 = acc[m][t][4 * g + 0] + bv.x, v1 = acc[m][t][4 * g + 1] + bv.y;
+        float v2 = acc[m][t][4 * g + 2] + bv.z, v3 = acc[m][t][4 * g + 3] + bv.w;
+        if (RESID) {
+          const bf16x4 x = *(const bf16x4 *)p;
+          v0 += (float)x[0];
+          v1 += (float)x[1];
+          v2 += (float)x[2];
+          v3 += (float)x[3];
+        }
+        bf16x4 o;
+        o[0] = (__bf16)fmaxf(v0, 0.f);
+        o[1] = (__bf16)fmaxf(v1, 0.f);
+        o[2] = (__bf16)fmaxf(v2, 0.f);
+        o[3] = (__bf16)fmaxf(v3, 0.f);
+        *(bf16x4 *)p = o;
+      }
+    }
+}
+
+// Packed-math form of acc_store_bias_relu: v_pk_add_f32 for bias (and residual), one
+// v_cvt_pk_bf16_f32 per pair, ReLU on the packed bf16 pair as a signed 16-bit max with 0
+// (v_pk_max_i16: a bf16 with the sign bit set is a negative int16).
+__device__ __forceinline__ uint32_t relu_pk_bf16(f32x2 v) {
+  const bf16x2 b = __builtin_convertvector(v, bf16x2);
+  const i16x2 m = __builtin_elementwise_max(__builtin_bit_cast(i16x2, b), i16x2{0, 0});
+  return __builtin_bit_cast(uint32_t, m);
+}
+
+template <class K, bool RESID>
+__device__ __forceinline__ void acc_store_bias_relu_pk(const f32x16 (&acc)[K::MT][K::NT], char *dst, const float *bias,
+                                                       int wave, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int m = 0; m < K::MT; ++m)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int ch = ((wave % K::CG) * K::MT + m) * 32 + 8 * g + 4 * h;
+      const float4 bv = *(const float4 *)(bias + ch);
+      const f32x2 b01 = {bv.x, bv.y}, b23 = {bv.z, bv.w};
+#pragma unroll
+      for (int t = 0; t < K::NT; ++t) {
+        char *p = dst + (((wave / K::CG) * K::NT + t) * 32 + r) * K::RS + ch * 2;
+        f32x2 lo = f32x2{acc[m][t][4 * g + 0], acc[m][t][4 * g + 1]} + b01;
+        f32x2 hi = f32x2{acc[m][t][4 * g + 2], acc[m][t][4 * g + 3]} + b23;
+        if (RESID) {
+          const uint2 x = *(const uint2 *)p;
+          lo += f32x2{__uint_as_float(x.x << 16), __uint_as_float(x.x & 0xffff0000u)};
+          hi += f32x2{__uint_as_float(x.y << 16), __uint_as_float(x.y & 0xffff0000u)};
+        }
+        *(uint2 *)p = make_uint2(relu_pk_bf16(lo), relu_pk_bf16(hi));
       }
     }
 }
@@ -154,8 +240,17 @@ __device__ __forceinline__ void conv_layer(const char *src, char *dst, const Nbr
   constexpr int STEPS = 9 * KK;
   static_assert(KK % DEPTH == 0, "ring slot must be a compile-time function of kk");
   const int h = lane >> 5;
+  constexpr bool ZINIT = (K::ABL & 64) == 0;  // first k-step from zero, bias/residual in the epilogue
   f32x16 acc[K::MT][K::NT];
-  acc_init<K, RESID>(acc, dst, bias, wave, lane);
+  if constexpr (ZINIT) {
+  } else if constexpr (K::ABL & 1) {
+#pragma unroll
+    for (int m = 0; m < K::MT; ++m)
+#pragma unroll
+      for (int t = 0; t < K::NT; ++t) acc[m][t] = f32x16{};
+  } else {
+    acc_init<K, RESID>(acc, dst, bias, wave, lane);
+  }
 
   const int hoff = 16 * h;  // byte offset of this lane's 8 channels inside a 16-channel k-step
   int off_cur[K::NT], off_nxt[K::NT];
@@ -173,7 +268,10 @@ __device__ __forceinline__ void conv_layer(const char *src, char *dst, const Nbr
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
       const int s = tap * KK + kk;
-      if (kk + 1 < KK) {
+      if constexpr (K::ABL & 8) {
+#pragma unroll
+        for (int t = 0; t < K::NT; ++t) bn[t] = bc[t];
+      } else if (kk + 1 < KK) {
 #pragma unroll
         for (int t = 0; t < K::NT; ++t) bn[t] = lds_b128(src + off_cur[t] + (kk + 1) * 32);
       } else if (tap + 1 < 9) {
@@ -185,7 +283,12 @@ __device__ __forceinline__ void conv_layer(const char *src, char *dst, const Nbr
 #pragma unroll
       for (int m = 0; m < K::MT; ++m) acur[m] = a[slot][m];
       const int sn = s + DEPTH;
-      if (sn < STEPS) {
+      if constexpr (K::ABL & 16) {
+      } else if constexpr (K::ABL & 128) {
+        if (sn < STEPS) a[slot][0] = wl[0][(size_t)sn * 64];
+#pragma unroll
+        for (int m = 1; m < K::MT; ++m) a[slot][m] = a[slot][0];
+      } else if (sn < STEPS) {
 #pragma unroll
         for (int m = 0; m < K::MT; ++m) a[slot][m] = wl[m][(size_t)sn * 64];
       } else if (sn - STEPS < wn_steps) {
@@ -193,12 +296,59 @@ __device__ __forceinline__ void conv_layer(const char *src, char *dst, const Nbr
         for (int m = 0; m < K::MT; ++m) a[slot][m] = wn[m][(size_t)(sn - STEPS) * 64];
       }
       // keep the prefetches ahead of this step's MFMAs (hipcc otherwise sinks them just-in-time)
-      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (K::ABL & 256) __builtin_amdgcn_sched_barrier(0);
+      if (ZINIT && s == 0) {
 #pragma unroll
-      for (int t = 0; t < K::NT; ++t)
+        for (int t = 0; t < K::NT; ++t)
 #pragma unroll
-        for (int m = 0; m < K::MT; ++m)
-          acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[m], bc[t], acc[m][t], 0, 0, 0);
+          for (int m = 0; m < K::MT; ++m)
+            acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[m], bc[t], f32x16{}, 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int t = 0; t < K::NT; ++t)
+#pragma unroll
+          for (int m = 0; m < K::MT; ++m)
+            acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[m], bc[t], acc[m][t], 0, 0, 0);
+      }
+      if constexpr (!(K::ABL & 256)) {
+        // interleave this step's loads (next B fragments, ring refill) between its MFMAs:
+        // one LDS read or global load per MFMA gap instead of a burst between MFMA blocks
+        if constexpr (K::ABL & 512) {  // global loads first
+#pragma unroll
+          for (int i = 0; i < K::MT; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+          }
+#pragma unroll
+          for (int i = 0; i < K::NT; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
+        } else if constexpr (K::ABL & 1024) {  // one global load per NT/MT LDS reads, spread
+#pragma unroll
+          for (int i = 0; i < K::MT; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+#pragma unroll
+            for (int j = 0; j < K::NT / K::MT; ++j) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < K::NT; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+          }
+#pragma unroll
+          for (int i = 0; i < K::MT; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+          }
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, K::MT * K::NT - K::NT - K::MT, 0);
+      }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int t = 0; t < K::NT; ++t) bc[t] = bn[t];
@@ -206,7 +356,15 @@ __device__ __forceinline__ void conv_layer(const char *src, char *dst, const Nbr
 #pragma unroll
     for (int t = 0; t < K::NT; ++t) off_cur[t] = off_nxt[t];
   }
-  acc_store_relu<K>(acc, dst, wave, lane);
+  if constexpr (K::ABL & 2) {
+    if (bias[0] == 12345.f) acc_store_relu<K>(acc, dst, wave, lane);  // keeps the MFMAs live
+  } else if constexpr (ZINIT && (K::ABL & 2048)) {
+    acc_store_bias_relu_pk<K, RESID>(acc, dst, bias, wave, lane);
+  } else if constexpr (ZINIT) {
+    acc_store_bias_relu<K, RESID>(acc, dst, bias, wave, lane);
+  } else {
+    acc_store_relu<K>(acc, dst, wave, lane);
+  }
 }
 
 // Stem: 3 input planes padded to one 16-channel k-step per tap (9 steps, weights loaded in place).
@@ -301,7 +459,7 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
   nb.init(lane & 31, wave / K::CG);
 
   // zero rows + stem input: Y rows hold 16 channels (3 planes, 13 zeros)
-  for (int i = tid; i < K::RS / 4; i += K::THREADS) {
+  for (int i = tid; i < K::NZ * K::RS / 4; i += K::THREADS) {
     ((uint32_t *)(X + K::ZROW * K::RS))[i] = 0u;
     ((uint32_t *)(Y + K::ZROW * K::RS))[i] = 0u;
   }
@@ -316,7 +474,7 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
   __syncthreads();
 
   constexpr int KK = K::C / 16;
-  constexpr int DEPTH = 4;
+  constexpr int DEPTH = K::DEPTH;
   constexpr size_t STEM = (size_t)K::C / 32 * 9 * 64;          // stem fragments
   constexpr size_t LAYER = (size_t)K::C / 32 * 9 * KK * 64;     // one block conv's fragments
   constexpr int LSTEPS = 9 * KK;
@@ -348,7 +506,7 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
     else
       conv_layer<K, KK, DEPTH, true>(Y, X, nb, wl, wn, wn_steps, ring, b, wave, lane);
     b += K::C;
-    __syncthreads();
+    if constexpr (!(K::ABL & 4)) __syncthreads();
   }
   const bf16x8 *w = wblk + (size_t)n_convs * LAYER;
   head_layer<K>(X, w, b, out, board0, batch, wave, lane);
@@ -628,6 +786,11 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
       case 5: return launch<Cfg<128, 256, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       case 8: return launch_split<Cfg<128, 256, 7, 6, 2, 8>, Cfg<128, 128, 7, 6, 2, 8>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       case 9: return launch_split<Cfg<128, 256, 7, 6, 4, 8>, Cfg<128, 128, 7, 6, 4, 8>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+#define ABLATE(X) \
+      case 100 + X: return launch<Cfg<128, 256, 7, 6, 2, 4, X>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      ABLATE(0) ABLATE(1) ABLATE(2) ABLATE(4) ABLATE(8) ABLATE(16) ABLATE(24) ABLATE(31) ABLATE(64) ABLATE(128)
+      ABLATE(256) ABLATE(2048)
+#undef ABLATE
       default: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
     }
   }
