@@ -25,6 +25,8 @@ import time
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
+TRAFFIC_FILE = os.path.join(HERE, "profiles", "r01_bench_prof", "k_tower_traffic.json")
+
 # MI355X reference figures (/opt/skills/guides/MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
 BF16_DENSE_PEAK_TFLOPS = 2500.0
@@ -185,6 +187,14 @@ def main():
     tw_flops_per_launch = rows * trunk_fpl / max(1, tw_launches)
     tw_avg_s = tw_ms / 1e3 / max(1, tw_launches)
     tw_tflops = tw_flops_per_launch / tw_avg_s / 1e12 if tw_avg_s > 0 else 0.0
+    # PMC-measured traffic of the same kernel on the same bench command (rocprofv3 FETCH_SIZE /
+    # WRITE_SIZE passes, scripts/gpu_prof_bench.sh -> scripts/pmc_traffic.py); bench.py cannot run
+    # the profiler itself, so it reports the committed measurement for the default workload
+    traffic, traffic_src = None, None
+    if os.path.exists(TRAFFIC_FILE) and (args.games, args.sims, args.filter_factor, args.blocks) == (4096, 200, 32, 20):
+        with open(TRAFFIC_FILE) as f:
+            traffic = json.load(f)["bytes_per_launch"]
+        traffic_src = os.path.relpath(TRAFFIC_FILE, HERE)
 
     out = {
         "metric": "self-play positions/sec (Connect4, 200 sims/move)",
@@ -215,7 +225,9 @@ def main():
             "peak": BF16_DENSE_PEAK_TFLOPS,
             "unit": "TFLOP/s",
             "frac": tw_tflops / BF16_DENSE_PEAK_TFLOPS,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_unit": "bytes/launch (L2<->fabric, PMC)",
+            "traffic_source": traffic_src,
             "flops_per_launch": tw_flops_per_launch,
             "flops_per_leaf": trunk_fpl,
             "avg_launch_us": tw_avg_s * 1e6,

@@ -1,5 +1,6 @@
 # rocprofv3 evidence for the bench: kernel-trace stats of the bench command, then separate
-# PMC passes (FETCH_SIZE, WRITE_SIZE) restricted to the dominant kernel (k_tower*).
+# PMC passes (FETCH_SIZE, WRITE_SIZE) restricted to the dominant kernel (k_tower*), reduced to
+# per-launch traffic by scripts/pmc_traffic.py.
 set -u
 mkdir -p gpurun_out/prof
 export TMPDIR=/tmp
@@ -9,11 +10,12 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof/tra
 rc=$?; echo "trace rc=$rc"; cut -c1-300 gpurun_out/prof/bench_traced.json
 if [ $rc -ne 0 ]; then tail -5 gpurun_out/prof/trace.err; exit $rc; fi
 i=0
-for set in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum"; do
+for set in "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
   timeout -k 10 600 rocprofv3 --pmc $set --kernel-include-regex "k_tower" -f csv -d gpurun_out/prof/pmc$i -o run -- \
      python3 bench.py $ARGS > gpurun_out/prof/pmc$i.json 2> gpurun_out/prof/pmc$i.err
   rc=$?; echo "pmc pass $i rc=$rc ($set)"
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/prof/pmc$i.err; exit $rc; fi
 done
-exit 0
+python3 scripts/pmc_traffic.py gpurun_out/prof/pmc1/run_counter_collection.csv \
+  gpurun_out/prof/pmc2/run_counter_collection.csv gpurun_out/prof/k_tower_traffic.json

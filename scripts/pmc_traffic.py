@@ -1,0 +1,31 @@
+"""Per-launch L2<->fabric traffic of the trunk kernel from rocprofv3 PMC passes (scripts/gpu_prof_bench.sh).
+
+FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of 16-B-per-lane
+streaming reads (MI355X_MICROARCH.md, HBM/rocprofv3 section), so reads are doubled.  Writes the
+JSON that bench.py reports as roofline.traffic.
+"""
+import csv
+import json
+import sys
+
+
+def mean_counter(path, name, kernel="k_tower_dyn"):
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+            if kernel in r["Kernel_Name"] and r["Counter_Name"] == name]
+    return sum(vals) / len(vals), len(vals)
+
+
+def main(fetch_csv, write_csv, out_json):
+    fetch, n = mean_counter(fetch_csv, "FETCH_SIZE")
+    write, _ = mean_counter(write_csv, "WRITE_SIZE")
+    res = dict(kernel="k_tower_dyn", launches=n, fetch_kib=fetch, write_kib=write,
+               read_bytes=2 * fetch * 1024, write_bytes=write * 1024,
+               bytes_per_launch=2 * fetch * 1024 + write * 1024,
+               note="FETCH_SIZE x2 (gfx950 16-B read correction) + WRITE_SIZE, KiB -> bytes; "
+                    "L2<->fabric traffic (Infinity Cache hits included)")
+    json.dump(res, open(out_json, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])
