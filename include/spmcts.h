@@ -241,8 +241,10 @@ int spmcts_tower_forward(int32_t width, int32_t height, int32_t channels, int32_
                          int32_t batch, const void *weights_dev, const float *bias_dev, void *features_dev,
                          spmcts_stream stream);
 /* The linear heads on the trunk features (modules.py:96-105), fused: policy softmax over
- * `actions` and tanh value.  head_w: bf16 [32 (policy, zero-padded)][K] ++ [8ff][K],
- * K = W*H*ff, columns in (cell, channel) order; head_b: f32 bp[32] ++ bv[8ff] ++ wo[8ff] ++ bo. */
+ * `actions` and tanh value.  head_w: bf16 rows [32 (policy, zero-padded)] ++ [8ff] over K = W*H*ff
+ * columns in (cell, channel) order, fragment-swizzled: for 32-row tile j and 16-column step s, one
+ * contiguous 1 KiB block whose 16-byte lane l holds row 32j + (l % 32), columns 16s + 8(l / 32) .. +8;
+ * head_b: f32 bp[32] ++ bv[8ff] ++ wo[8ff] ++ bo. */
 int spmcts_tower_heads(int32_t width, int32_t height, int32_t channels, int32_t actions, const void *features_dev,
                        int32_t batch, const void *head_w_dev, const float *head_b_dev, float *probs_dev,
                        float *values_dev, spmcts_stream stream);

@@ -547,66 +547,100 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 }
 
 // ---------------------------------------------------------------------------------------
-// Linear heads (modules.py:96-105 after the 1x1 convs), fused: for 32 boards per workgroup
+// Linear heads (modules.py:96-105 after the 1x1 convs), fused, for BOARDS boards per workgroup:
 //   policy = softmax(pf @ Wp^T + bp)          pf = features[:, :, :ff]  (cell-major, K = cells*ff)
 //   value  = tanh(relu(vf @ Wv^T + bv) @ wo + bo)                     vf = features[:, :, ff:]
-// on v_mfma_f32_32x32x16_bf16 with M = 32 boards.  Weight blob (bf16): Wp padded to 32 rows
-// [32][K] then Wv [8ff][K]; float blob: bp[32] (padded), bv[8ff], wo[8ff], bo.
+// on v_mfma_f32_32x32x16_bf16 (M = 32 rows of which BOARDS are boards, N = 32 weight rows).
+// The workgroup's features are staged once into LDS (coalesced; per-board stride padded by 16 B
+// so the 16-B operand reads of 16 different boards are bank-conflict free); weight fragments are
+// pre-swizzled on the host (one contiguous KiB per (32-row tile, 16-k step): lane (r, h) holds
+// W[tile*32 + r][16 s + 8 h .. + 8]) and streamed through a 4-deep register ring.  Wave w owns
+// value tiles [w*VTW, (w+1)*VTW) over all of K and the policy tile over a quarter of K; partial
+// sums are combined in a fixed order (deterministic, batch-independent).
+// Weight blob: tile 0 = Wp padded to 32 rows, tiles 1..VT = Wv; float blob: bp[32], bv[8ff], wo[8ff], bo.
 template <int FF, int CELLS, int A>
-__global__ __launch_bounds__(256) void k_heads(const __bf16 *feats, int n, const int32_t *count, const __bf16 *hw,
+struct HeadsCfg {
+  static constexpr int K = CELLS * FF, KS = K / 16, HID = 8 * FF, VT = HID / 32, VTW = VT / 4;
+  static constexpr int FROW = CELLS * 2 * FF * 2;  // feature bytes per board
+  static constexpr int BOARDS = FROW * 16 + 16 * 16 <= 96 * 1024 ? 16 : 8;
+  static constexpr int FS = FROW + 16;             // LDS stride per board
+  static constexpr int KQ = (KS + 3) / 4;          // policy k-steps per wave
+  static_assert(VT % 4 == 0 && FF % 16 == 0 && FROW % 16 == 0, "head tile plan");
+};
+
+template <int FF, int CELLS, int A>
+__global__ __launch_bounds__(256) void k_heads(const __bf16 *feats, int n, const int32_t *count, const bf16x8 *wf,
                                                const float *hb, float *probs, float *values) {
+  using H = HeadsCfg<FF, CELLS, A>;
   if (count) n = *count;
-  if ((int)blockIdx.x * 32 >= n) return;
-  constexpr int K = CELLS * FF;
-  constexpr int KS = K / 16;
-  constexpr int HID = 8 * FF;
-  constexpr int VT = HID / 32;       // value hidden tiles
-  constexpr int VTW = VT / 4;        // per wave
-  static_assert(VT % 4 == 0 && FF % 16 == 0, "head tile plan");
-  __shared__ float s_part[4][32];  // per-wave value partial sums (fixed-order reduction: deterministic)
-  __shared__ float s_logit[32][33];
+  const int b0 = blockIdx.x * H::BOARDS;
+  if (b0 >= n) return;
+  __shared__ __attribute__((aligned(16))) char s_feat[H::BOARDS * H::FS];
+  __shared__ float s_part[4][32];        // per-wave value partial sums
+  __shared__ float s_pol[4][32][33];     // per-wave policy partial logits
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
-  const int b0 = blockIdx.x * 32;
-  const __bf16 *wp = hw;
-  const __bf16 *wv = hw + (size_t)32 * K;
-  const float *bp = hb, *bv = hb + 32, *wo = hb + 32 + HID, *bo = hb + 32 + 2 * HID;
-  const int board = b0 + r;
-  const bool ok = board < n;
-  const __bf16 *frow = feats + (size_t)(ok ? board : 0) * CELLS * 2 * FF;
-  f32x16 acc[VTW];
-  f32x16 pacc;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) pacc[i] = 0.f;
-#pragma unroll
-  for (int v = 0; v < VTW; ++v)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[v][i] = 0.f;
-  const bf16x8 zero8 = {};
-  for (int s = 0; s < KS; ++s) {
-    const int k0 = 16 * s + 8 * h;
-    const int cell = k0 / FF, c = k0 % FF;
-    const bf16x8 av = ok ? *(const bf16x8 *)(frow + cell * 2 * FF + FF + c) : zero8;
-#pragma unroll
-    for (int v = 0; v < VTW; ++v) {
-      const int col = (wave * VTW + v) * 32 + r;
-      const bf16x8 bw = *(const bf16x8 *)(wv + (size_t)col * K + k0);
-      acc[v] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bw, acc[v], 0, 0, 0);
-    }
-    if (wave == 0) {
-      const bf16x8 ap = ok ? *(const bf16x8 *)(frow + cell * 2 * FF + c) : zero8;
-      const bf16x8 bw = *(const bf16x8 *)(wp + (size_t)r * K + k0);
-      pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap, bw, pacc, 0, 0, 0);
+  const int nb = min(H::BOARDS, n - b0);
+  // stage the features of this workgroup's boards (16 B per thread-iteration, coalesced)
+  {
+    constexpr int CH = H::FROW / 16;
+    const uint4 *src = (const uint4 *)(feats + (size_t)b0 * CELLS * 2 * FF);
+    for (int i = tid; i < H::BOARDS * CH; i += 256) {
+      const int bd = i / CH, c = i % CH;
+      const uint4 v = bd < nb ? src[(size_t)bd * CH + c] : make_uint4(0, 0, 0, 0);
+      *(uint4 *)(s_feat + bd * H::FS + c * 16) = v;
     }
   }
+  const float *bp = hb, *bv = hb + 32, *wo = hb + 32 + H::HID, *bo = hb + 32 + 2 * H::HID;
+  const int row = r % H::BOARDS;  // rows >= BOARDS duplicate a board; their results are ignored
+  const char *frow = s_feat + row * H::FS;
+  f32x16 acc[H::VTW];
+  f32x16 pacc = {};
+#pragma unroll
+  for (int v = 0; v < H::VTW; ++v) acc[v] = f32x16{};
+  // weight ring: VTW value fragments (+ 1 policy fragment while s is in this wave's quarter)
+  constexpr int D = 4;
+  bf16x8 ring[D][H::VTW];
+  const bf16x8 *wv = wf + (size_t)(1 + wave * H::VTW) * H::KS * 64 + lane;
+  const bf16x8 *wp = wf + lane;
+  const int q0 = wave * H::KQ, q1 = min(H::KS, q0 + H::KQ);
   __syncthreads();
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+#pragma unroll
+    for (int v = 0; v < H::VTW; ++v) ring[d][v] = wv[((size_t)v * H::KS + d) * 64];
+  bf16x8 pnext = wp[(size_t)q0 * 64];
+  for (int s0 = 0; s0 < H::KS; s0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int s = s0 + d;
+      if (s >= H::KS) break;
+      const int k0 = 16 * s + 8 * h;
+      const int cell = k0 / FF, c = k0 % FF;
+      const bf16x8 av = *(const bf16x8 *)(frow + (cell * 2 * FF + FF + c) * 2);
+      bf16x8 wcur[H::VTW];
+#pragma unroll
+      for (int v = 0; v < H::VTW; ++v) {
+        wcur[v] = ring[d][v];
+        if (s + D < H::KS) ring[d][v] = wv[((size_t)v * H::KS + s + D) * 64];
+      }
+#pragma unroll
+      for (int v = 0; v < H::VTW; ++v) acc[v] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, wcur[v], acc[v], 0, 0, 0);
+      if (s >= q0 && s < q1) {
+        const bf16x8 ap = *(const bf16x8 *)(frow + (cell * 2 * FF + c) * 2);
+        const bf16x8 pw = pnext;
+        if (s + 1 < q1) pnext = wp[(size_t)(s + 1) * 64];
+        pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap, pw, pacc, 0, 0, 0);
+      }
+    }
+  }
   // value: relu(acc + bv[col]) * wo[col], summed over the hidden units (cols)
   // D layout: lane (r, h): col = r, rows (boards) = (i & 3) + 8 * (i >> 2) + 4 * h
   float part[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) part[i] = 0.f;
 #pragma unroll
-  for (int v = 0; v < VTW; ++v) {
-    const int col = (wave * VTW + v) * 32 + r;
+  for (int v = 0; v < H::VTW; ++v) {
+    const int col = (wave * H::VTW + v) * 32 + r;
     const float bb = bv[col], ww = wo[col];
 #pragma unroll
     for (int i = 0; i < 16; ++i) part[i] += fmaxf(acc[v][i] + bb, 0.f) * ww;
@@ -622,28 +656,28 @@ __global__ __launch_bounds__(256) void k_heads(const __bf16 *feats, int n, const
 #pragma unroll
     for (int i = 0; i < 16; ++i) s_part[wave][(i & 3) + 8 * (i >> 2) + 4 * h] = part[i];
   }
-  if (wave == 0) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) s_logit[(i & 3) + 8 * (i >> 2) + 4 * h][r] = pacc[i] + bp[r];
-  }
+  for (int i = 0; i < 16; ++i) s_pol[wave][(i & 3) + 8 * (i >> 2) + 4 * h][r] = pacc[i];
   __syncthreads();
-  if (tid < 32) {
+  if (tid < nb) {
     const int bd = b0 + tid;
-    if (bd < n) {
-      values[bd] = tanhf(((s_part[0][tid] + s_part[1][tid]) + (s_part[2][tid] + s_part[3][tid])) + bo[0]);
-      float m = -INFINITY;
+    values[bd] = tanhf(((s_part[0][tid] + s_part[1][tid]) + (s_part[2][tid] + s_part[3][tid])) + bo[0]);
+    float lg[A];
+    float m = -INFINITY;
 #pragma unroll
-      for (int a = 0; a < A; ++a) m = fmaxf(m, s_logit[tid][a]);
-      float e[A], sum = 0.f;
-#pragma unroll
-      for (int a = 0; a < A; ++a) {
-        e[a] = __expf(s_logit[tid][a] - m);
-        sum += e[a];
-      }
-      const float inv = 1.f / sum;
-#pragma unroll
-      for (int a = 0; a < A; ++a) probs[(size_t)bd * A + a] = e[a] * inv;
+    for (int a = 0; a < A; ++a) {
+      lg[a] = ((s_pol[0][tid][a] + s_pol[1][tid][a]) + (s_pol[2][tid][a] + s_pol[3][tid][a])) + bp[a];
+      m = fmaxf(m, lg[a]);
     }
+    float e[A], sum = 0.f;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      e[a] = __expf(lg[a] - m);
+      sum += e[a];
+    }
+    const float inv = 1.f / sum;
+#pragma unroll
+    for (int a = 0; a < A; ++a) probs[(size_t)bd * A + a] = e[a] * inv;
   }
 }
 
@@ -810,10 +844,11 @@ static int tower_heads(int32_t width, int32_t height, int32_t channels, int32_t 
   using namespace tower;
   hipStream_t s = (hipStream_t)stream;
   if (batch <= 0) return batch < 0 ? -3 : 0;
-  const int grid = (batch + 31) / 32;
 #define HEADS(FF, CELLS, A)                                                                                   \
-  hipLaunchKernelGGL((k_heads<FF, CELLS, A>), dim3(grid), dim3(256), 0, s, (const __bf16 *)features_dev, batch, \
-                     count_dev, (const __bf16 *)head_w_dev, head_b_dev, probs_dev, values_dev)
+  hipLaunchKernelGGL((k_heads<FF, CELLS, A>), dim3((batch + HeadsCfg<FF, CELLS, A>::BOARDS - 1) /             \
+                                                   HeadsCfg<FF, CELLS, A>::BOARDS), dim3(256), 0, s,           \
+                     (const __bf16 *)features_dev, batch, count_dev, (const bf16x8 *)head_w_dev, head_b_dev,    \
+                     probs_dev, values_dev)
   if (width == 7 && height == 6 && actions == 7 && channels == 128)
     HEADS(32, 42, 7);
   else if (width == 7 && height == 6 && actions == 7 && channels == 256)

@@ -253,7 +253,11 @@ class HipTowerEvaluator(Evaluator):
         K = cells * ff
         wp = torch.zeros(32, K, dtype=bf, device=dev)
         wp[: self.A] = self.lp_w
-        self.head_w = torch.cat([wp.reshape(-1), self.fv_w.reshape(-1)]).contiguous()
+        # fragment swizzle: tile j (0 = policy padded to 32 rows, 1.. = value hidden rows), k-step s,
+        # lane (r, h) -> W[32 j + r][16 s + 8 h .. + 8]: one contiguous KiB per (tile, k-step)
+        wall = torch.cat([wp, self.fv_w], 0)
+        nt, ks = wall.shape[0] // 32, K // 16
+        self.head_w = wall.view(nt, 32, ks, 2, 8).permute(0, 2, 3, 1, 4).contiguous().reshape(-1)
         bp = torch.zeros(32, dtype=torch.float32, device=dev)
         bp[: self.A] = t.linear_policy.bias.detach().float().to(dev)
         self.head_b = torch.cat([bp, t.fc_value.bias.detach().float().to(dev),
