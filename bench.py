@@ -15,6 +15,12 @@ rank 0 (the replay owner), as in the north star.
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
 Prints ONE JSON line on rank 0.
+
+Secondary workloads (BASELINE.json configs; not the headline line):
+  --sims 800 --games 16384 --filter-factor 64   config 3 (deep trees, ResNet-256)
+  --mode arena --games 8192                     config 5: arena evaluation, two frozen nets
+                                                (seeds 0 / 1), evaluate mode, no Move records;
+                                                metric = games finished per second
 """
 import argparse
 import json
@@ -112,7 +118,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="skip the rank-0 Move gather")
+    ap.add_argument("--mode", choices=["selfplay", "arena"], default="selfplay")
     args = ap.parse_args()
+    arena_mode = args.mode == "arena"
 
     import torch
 
@@ -126,8 +134,13 @@ def main():
 
     torch.manual_seed(0)
     net = ResidualTower(7, 6, 7, num_blocks=args.blocks, filter_factor=args.filter_factor).to(dev).eval()
+    opponent = None
+    if arena_mode:  # BASELINE config 5: two frozen nets, greedy (evaluate-mode) MCTS on both sides
+        torch.manual_seed(1)
+        opponent = ResidualTower(7, 6, 7, num_blocks=args.blocks, filter_factor=args.filter_factor).to(dev).eval()
     eng = SelfPlayEngine("connect4", net, n_games=args.games, iterations=args.sims, seed=1234 + rank,
-                         device=dev, bucket=args.bucket)
+                         device=dev, bucket=args.bucket, opponent=opponent, evaluate=arena_mode,
+                         record=not arena_mode)
     gathered = []
 
     def on_moves(m):
@@ -139,7 +152,7 @@ def main():
             gathered.append(int(m["z"].shape[0]))
 
     def one_step():
-        eng.ply(on_moves=on_moves if not args.no_gather else None)
+        eng.ply(on_moves=on_moves if not (args.no_gather or arena_mode) else None)
         D.all_reduce_stats(eng.stats_vector())  # episode-end statistics exchange
 
     for _ in range(args.warmup):
@@ -219,7 +232,7 @@ def main():
             "parallelism": f"dp{world}",
         },
         "roofline": {
-            "kernel": "tower::k_tower_dyn (fused ResNet-128x20 trunk, bf16 MFMA)",
+            "kernel": f"tower::k_tower_dyn (fused ResNet-{4 * args.filter_factor}x{args.blocks} trunk, bf16 MFMA)",
             "bound": "mfma",
             "achieved": tw_tflops,
             "peak": BF16_DENSE_PEAK_TFLOPS,
@@ -264,6 +277,15 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if arena_mode:
+        out["metric"] = f"arena evaluation games/sec (Connect4, {args.sims} sims/move, two frozen nets)"
+        out["value"] = games_all / elapsed_max
+        out["unit"] = "games/s"
+        out["positions_per_s"] = moves_all / elapsed_max
+        out["config"]["workload"] = (f"connect4 7x6 arena evaluation, {args.sims} sims/move, {args.games} concurrent "
+                                     f"games per GPU, policy ResNet-{4 * args.filter_factor}x{args.blocks} (seed 0) vs "
+                                     f"opponent (seed 1), evaluate mode (temp/20, noise on), no Move records")
+        args.no_cpu_baseline = True
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cores = min(16, os.cpu_count() or 1)
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, cores, args.sims, args.filter_factor, args.blocks)

@@ -138,7 +138,9 @@ class SelfPlayEngine:
         self.select_timer = EventTimer() if on else None
         self.nn_timer = EventTimer() if on else None
         self.tower_timer = EventTimer() if on else None
-        self.evaluator.tower_timer = self.tower_timer
+        for ev in (self.evaluator, self.evaluator1):
+            if ev is not None:
+                ev.tower_timer = self.tower_timer
 
     def start(self):
         """Fill every slot and keep refilling (until `max_games` games have started, if set)."""
