@@ -35,8 +35,9 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef short i16x2 __attribute__((ext_vector_type(2)));
 
 
-template <int C_, int ROWS_, int W_, int H_, int CG_ = 2, int WAVES_ = 4, int ABL_ = 0, int DEPTH_ = 4>
+template <int C_, int ROWS_, int W_, int H_, int CG_ = 2, int WAVES_ = 4, int ABL_ = 0, int DEPTH_ = 4, int OCC_ = 1>
 struct Cfg {
+  static constexpr int OCC = OCC_;  // resident workgroups per CU the register budget is sized for
   static constexpr int DEPTH = DEPTH_;  // weight-fragment prefetch distance (k-steps)
   static constexpr int C = C_, ROWS = ROWS_, W = W_, H = H_;
   // ABL: timing ablations for kernel analysis only (results are wrong): 1 = no accumulator init,
@@ -513,7 +514,7 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
 }
 
 template <class K>
-__global__ __launch_bounds__(K::THREADS) __attribute__((amdgpu_waves_per_eu(K::WAVES / 4, K::WAVES / 4))) void k_tower(
+__global__ __launch_bounds__(K::THREADS) __attribute__((amdgpu_waves_per_eu(K::WAVES / 4 * K::OCC, K::WAVES / 4 * K::OCC))) void k_tower(
     const __bf16 *planes, int batch, int n_blocks, const bf16x8 *wpk, const float *bias, __bf16 *out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   tower_tile<K>(smem, planes, batch, blockIdx.x * K::BOARDS, n_blocks, wpk, bias, out);
@@ -825,6 +826,11 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
       ABLATE(0) ABLATE(1) ABLATE(2) ABLATE(4) ABLATE(8) ABLATE(16) ABLATE(24) ABLATE(31) ABLATE(64) ABLATE(128)
       ABLATE(256) ABLATE(2048)
 #undef ABLATE
+      case 20: return launch<Cfg<128, 128, 7, 6, 2, 4, 0, 4, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      case 21: return launch<Cfg<128, 128, 7, 6, 4, 4, 0, 4, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      case 22: return launch<Cfg<128, 128, 7, 6, 2, 4, 0, 2, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      case 23: return launch<Cfg<128, 256, 7, 6, 4, 4, 0, 8>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      case 24: return launch<Cfg<128, 256, 7, 6, 4, 4, 0, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       default: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
     }
   }
