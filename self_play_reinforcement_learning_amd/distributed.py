@@ -35,9 +35,11 @@ def env_rank():
 def init_from_env(backend=None):
     """Initialise torch.distributed from torchrun's environment (no-op for world size 1)."""
     rank, world, local = env_rank()
+    if torch.cuda.is_available() and torch.cuda.device_count() > 0:
+        local = local % torch.cuda.device_count()  # (rehearsals: several ranks on a 1-GPU box)
     if world > 1 and not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = os.environ.get("SPMCTS_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         kw = {}
@@ -48,6 +50,13 @@ def init_from_env(backend=None):
     elif torch.cuda.is_available():
         torch.cuda.set_device(local)
     return rank, world, local
+
+
+def local_device():
+    """This rank's GPU (LOCAL_RANK, wrapped onto the visible devices)."""
+    local = env_rank()[2]
+    n = torch.cuda.device_count() if torch.cuda.is_available() else 0
+    return torch.device("cuda", local % n) if n else torch.device("cpu")
 
 
 def is_distributed():
@@ -76,6 +85,15 @@ def all_reduce_stats(stats):
     return t.cpu()
 
 
+def all_ranks_true(flag):
+    """True iff `flag` holds on every rank (an all_reduce MIN; local value without a process group)."""
+    if not is_distributed():
+        return bool(flag)
+    t = torch.tensor([1 if flag else 0], dtype=torch.int64, device=_comm_device())
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
 def all_reduce_max(value):
     t = torch.tensor([float(value)], dtype=torch.float64)
     if not is_distributed():
@@ -95,8 +113,12 @@ def pack_moves(moves):
     n = moves["z"].shape[0]
     cols = []
     for name, dt in _FIELDS:
-        t = moves[name].to(dt).reshape(n, -1).contiguous()
-        cols.append(t.view(torch.uint8).reshape(n, -1))
+        t = moves[name].to(dt)
+        per_row = 1
+        for d in t.shape[1:]:
+            per_row *= int(d)
+        t = t.reshape(n, per_row).contiguous()  # explicit width: n may be 0
+        cols.append(t.view(torch.uint8).reshape(n, per_row * t.element_size()))
     return torch.cat(cols, dim=1)
 
 
@@ -105,7 +127,7 @@ def unpack_moves(rows, cells, n_actions):
     out, off = {}, 0
     for name, dt in _FIELDS:
         w = widths[name]
-        chunk = rows[:, off:off + w].contiguous()
+        chunk = torch.empty((rows.shape[0], w), dtype=torch.uint8).copy_(rows[:, off:off + w])  # fresh, offset 0
         t = chunk.view(dt)
         out[name] = t if name in ("state", "tree_probs") else t.reshape(-1)
         off += w

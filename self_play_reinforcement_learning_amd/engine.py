@@ -231,6 +231,9 @@ class SelfPlayEngine:
             exported = int(moves["z"].shape[0])
             if on_moves is not None:
                 on_moves(moves)
+        elif on_moves is not None and distributed.is_distributed():
+            # every rank takes part in the per-ply collectives in on_moves, with or without records
+            on_moves(a.export_moves(0))
         self.games_done += finished
         self.positions += exported
         self.plies += 1
@@ -261,22 +264,23 @@ class SelfPlayEngine:
         """Play exactly `n` more games (refilling slots on device until n have started).
 
         Returns the number of plies it took.  Game ids continue from earlier calls, so
-        swap_sides alternates across calls exactly as the reference's task ids do."""
+        swap_sides alternates across calls exactly as the reference's task ids do.
+        Under torch.distributed every rank plays its own `n` and keeps stepping (idle plies)
+        until all ranks are done, so the per-ply collectives in on_moves / on_ply stay matched."""
         a = self.arena
-        if n <= 0:
-            return 0
         started = getattr(self, "_started", 0)
-        limit = started + n
-        a.games_set_limit(limit)
-        st = a.games_state()
-        idle = [i for i, s in enumerate(st["state"]) if s == 0]
-        k = min(len(idle), n)
-        if k:
-            a.games_start(idle[:k])
-        self.started = True
-        target = self.games_done + n
+        limit = started + max(0, n)
+        if n > 0:
+            a.games_set_limit(limit)
+            st = a.games_state()
+            idle = [i for i, s in enumerate(st["state"]) if s == 0]
+            k = min(len(idle), n)
+            if k:
+                a.games_start(idle[:k])
+            self.started = True
+        target = self.games_done + max(0, n)
         plies = 0
-        while self.games_done < target:
+        while not distributed.all_ranks_true(self.games_done >= target):
             self.ply(on_moves=on_moves)
             plies += 1
             if on_ply is not None:

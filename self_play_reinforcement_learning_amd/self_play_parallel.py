@@ -104,8 +104,7 @@ class SelfPlayScheduler:
         self.updates_per_ply = updates_per_ply
         rank, world, local = D.env_rank()
         self.rank, self.world = rank, world
-        self.device = torch.device(device) if device is not None else torch.device(
-            "cuda", local if torch.cuda.is_available() else 0)
+        self.device = torch.device(device) if device is not None else D.local_device()
         self.n_games = n_games
         self.start_time = datetime.datetime.now().isoformat()
         self.task_queue = LocalQueue()

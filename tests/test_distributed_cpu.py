@@ -46,6 +46,71 @@ def _worker(rank, world, port, q):
     torch.distributed.destroy_process_group()
 
 
+class _FakeArena:
+    def __init__(self, slots):
+        self.slots = slots
+
+    def games_set_limit(self, n):
+        self.limit = n
+
+    def games_state(self):
+        import numpy as np
+
+        return {"state": np.zeros(self.slots, dtype=int)}
+
+    def games_start(self, slots):
+        self.started = list(slots)
+
+
+class _FakeEngine:
+    """Stands in for SelfPlayEngine inside its own play_games loop: rank r finishes r + 1 games per
+    ply, and every ply runs the same per-ply collectives as the scheduler (gather + stats)."""
+
+    def __init__(self, rate):
+        self.arena = _FakeArena(4)
+        self.games_done = 0
+        self.rate = rate
+        self.plies_run = 0
+
+    def ply(self, on_moves=None):
+        self.plies_run += 1
+        self.games_done += self.rate
+        on_moves(_moves(0, 0))
+
+
+def _loop_worker(rank, world, port, q):
+    from self_play_reinforcement_learning_amd.engine import SelfPlayEngine
+
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    D.init_from_env(backend="gloo")
+    eng = _FakeEngine(rate=rank + 1)
+    gathered = []
+    plies = SelfPlayEngine.play_games(
+        eng, 6, on_moves=lambda m: gathered.append(D.gather_moves(m, 42, 7)),
+        on_ply=lambda e: D.all_reduce_stats([e.games_done]))
+    q.put((rank, plies, eng.games_done, len(gathered)))
+    torch.distributed.destroy_process_group()
+
+
+def test_play_games_keeps_ranks_in_step_gloo():
+    """Ranks that finish their share early keep stepping until every rank is done, so the
+    per-ply collectives (Move gather, stats all_reduce) always match (no deadlock)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_loop_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in procs], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, p0, d0, g0), (r1, p1, d1, g1) = res
+    assert p0 == p1 == 6 and g0 == g1 == 6  # rank 0 needs 6 plies for its 6 games; rank 1 idles along
+    assert d0 == 6 and d1 == 12
+
+
 def test_pack_unpack_roundtrip():
     m = _moves(0, 9)
     back = D.unpack_moves(D.pack_moves(m), 42, 7)
