@@ -66,43 +66,55 @@ def select_bytes(sims, levels, A=7):
     return levels * per_level + sims * per_sim
 
 
-def cpu_baseline(seconds, cores, sims, filter_factor, num_blocks):
-    """The oracle (sequential Python MCTS restatement, numpy RNG) + the reference-architecture
-    ResNet in fp32 on host cores: one Connect4 game from the empty board, complete moves
-    only, for about `seconds`.  Same tree semantics as the reference's sequential search
-    (games/algos/mcts.py); no multiprocessing/IPC."""
+def _cpu_worker(args):
+    """One host process: the oracle's sequential search (the reference's MCTreeSearch algorithm,
+    numpy RNG) + the reference-architecture ResNet in fp32 torch on ONE thread, Connect4 games
+    from the empty board, complete moves only, for `seconds`."""
+    seconds, seed, sims, filter_factor, num_blocks = args
     import numpy as np
     import torch
 
+    from oracle.envs import Connect4Env
     from oracle.mcts import NumpyRNG, OracleTree
     from self_play_reinforcement_learning_amd.modules import ResidualTower
 
-    torch.set_num_threads(cores)
+    torch.set_num_threads(1)
     torch.manual_seed(0)
     net = ResidualTower(7, 6, 7, num_blocks=num_blocks, filter_factor=filter_factor).eval()
-    np.random.seed(0)
+    np.random.seed(seed)
+    moves = 0
     with torch.no_grad():
-        tree = OracleTree("connect4", net, NumpyRNG(), sims)
-        env_player = 1
-        from oracle.envs import Connect4Env
-
-        env = Connect4Env()
+        tree, env, player = OracleTree("connect4", net, NumpyRNG(), sims), Connect4Env(), 1
         t0 = time.time()
-        moves = 0
         while time.time() - t0 < seconds:
             a = tree.move()
             tree.play_action(a)
-            _, r, done, _ = env.step(a, env_player)
+            _, _, done, _ = env.step(a, player)
             moves += 1
-            env_player = -env_player
+            player = -player
             if done:
                 env.reset()
-                tree = OracleTree("connect4", net, NumpyRNG(), sims)
-                env_player = 1
+                tree, player = OracleTree("connect4", net, NumpyRNG(), sims), 1
         dt = time.time() - t0
-    return dict(value=moves / dt, unit="positions/s", cores=cores, kind="port",
-                sample=f"oracle sequential MCTS ({sims} sims/move, numpy RNG) + ResNet-{4 * filter_factor}x{num_blocks} "
-                       f"fp32 torch CPU, 1 Connect4 game from the empty board, {moves} complete moves in {dt:.1f} s")
+    return moves, dt
+
+
+def cpu_baseline(seconds, cores, sims, filter_factor, num_blocks):
+    """The reference's CPU self-play structure restated: `cores` independent play processes (the
+    reference runs one SelfPlayWorker per core, self_play_parallel.py:95-171), each running the
+    oracle's sequential search with a 1-thread fp32 ResNet, for about `seconds`; positions/s summed
+    over processes.  (No IPC inference batching: the reference's proxy adds queue round trips.)"""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(cores) as pool:
+        res = pool.map(_cpu_worker, [(seconds, 1000 + i, sims, filter_factor, num_blocks) for i in range(cores)])
+    moves = sum(m for m, _ in res)
+    rate = sum(m / dt for m, dt in res)
+    return dict(value=rate, unit="positions/s", cores=cores, kind="port",
+                sample=f"{cores} processes x (oracle sequential MCTS, {sims} sims/move, numpy RNG + ResNet-"
+                       f"{4 * filter_factor}x{num_blocks} fp32 torch, 1 thread), Connect4 games from the empty board, "
+                       f"{moves} complete moves in ~{seconds:.0f} s")
 
 
 def main():
@@ -121,6 +133,13 @@ def main():
     ap.add_argument("--mode", choices=["selfplay", "arena"], default="selfplay")
     args = ap.parse_args()
     arena_mode = args.mode == "arena"
+
+    # The CPU baseline runs FIRST, in child processes started before this process touches the GPU
+    # (children of a GPU-initialised process must not exec); rank 0 of a 1-process run only.
+    env_rank, env_world = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
+    cpu = None
+    if env_rank == 0 and env_world == 1 and not args.no_cpu_baseline and not arena_mode:
+        cpu = cpu_baseline(args.cpu_seconds, min(16, os.cpu_count() or 1), args.sims, args.filter_factor, args.blocks)
 
     import torch
 
@@ -285,10 +304,7 @@ def main():
         out["config"]["workload"] = (f"connect4 7x6 arena evaluation, {args.sims} sims/move, {args.games} concurrent "
                                      f"games per GPU, policy ResNet-{4 * args.filter_factor}x{args.blocks} (seed 0) vs "
                                      f"opponent (seed 1), evaluate mode (temp/20, noise on), no Move records")
-        args.no_cpu_baseline = True
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cores = min(16, os.cpu_count() or 1)
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, cores, args.sims, args.filter_factor, args.blocks)
+    out["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(out), flush=True)
     if D.is_distributed():
