@@ -45,7 +45,8 @@ struct Cfg {
   // 16 = no weight loads in the k-loop, 128 = half the weight loads (m = 0 only).
   // Schedule/epilogue alternatives (correct results): 64 = accumulator init with bias/residual
   // (instead of a zero first k-step and bias/residual in the epilogue), 256 = loads issued in a
-  // burst between MFMA blocks (instead of one per MFMA gap), 2048 = packed-math epilogue.
+  // burst between MFMA blocks (instead of one per MFMA gap), 2048 = packed-math epilogue,
+  // 32768 = weight ring through 64-bit global addresses (instead of a buffer resource).
   static constexpr int ABL = ABL_;
   static constexpr int WAVES = WAVES_, THREADS = 64 * WAVES_;
   static constexpr int CG = CG_;            // waves split output channels into CG groups ...
@@ -71,6 +72,19 @@ struct Cfg {
 };
 
 __device__ __forceinline__ bf16x8 lds_b128(const char *p) { return *(const bf16x8 *)p; }
+
+// Weight fragments through a buffer resource: the per-lane part of the address is a constant
+// 32-bit voffset (lane * 16) and the fragment's byte offset is a wave-uniform soffset, so a ring
+// refill is one buffer_load_dwordx4 with no per-load 64-bit address arithmetic.
+struct WBuf {
+  __amdgpu_buffer_rsrc_t rsrc;
+  int voff;
+  __device__ __forceinline__ bf16x8 load(uint32_t byte_off) const {
+    typedef int i32x4 __attribute__((ext_vector_type(4)));
+    const i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, (int)byte_off, 0);
+    return __builtin_bit_cast(bf16x8, v);
+  }
+};
 
 // One conv layer over the resident tile: src (LDS) -> dst (LDS), optional residual (LDS, == dst).
 // KK = input channels / 16 (k-steps per tap), TAPS = 9 (3x3).
@@ -237,7 +251,11 @@ __device__ __forceinline__ void acc_store_relu(const f32x16 (&acc)[K::MT][K::NT]
 template <class K, int KK, int DEPTH, bool RESID>
 __device__ __forceinline__ void conv_layer(const char *src, char *dst, const Nbr<K> &nb, const bf16x8 *const (&wl)[K::MT],
                                            const bf16x8 *const (&wn)[K::MT], int wn_steps, bf16x8 (&a)[DEPTH][K::MT],
-                                           const float *bias, int wave, int lane) {
+                                           const float *bias, int wave, int lane, const WBuf &wb, uint32_t wl_off,
+                                           uint32_t wn_off) {
+  // wl_off / wn_off: byte offset of (this layer / next layer, this wave's first channel tile, step 0);
+  // channel tile m adds m * 9 * KK fragments of 1 KiB, step s adds s KiB
+  constexpr uint32_t MSTRIDE = 9u * KK * 1024u;
   constexpr int STEPS = 9 * KK;
   static_assert(KK % DEPTH == 0, "ring slot must be a compile-time function of kk");
   const int h = lane >> 5;
@@ -289,6 +307,15 @@ __device__ __forceinline__ void conv_layer(const char *src, char *dst, const Nbr
         if (sn < STEPS) a[slot][0] = wl[0][(size_t)sn * 64];
 #pragma unroll
         for (int m = 1; m < K::MT; ++m) a[slot][m] = a[slot][0];
+      } else if constexpr (!(K::ABL & 32768)) {
+        if (sn < STEPS) {
+#pragma unroll
+          for (int m = 0; m < K::MT; ++m) a[slot][m] = wb.load(wl_off + m * MSTRIDE + (uint32_t)sn * 1024u);
+        } else if (sn - STEPS < wn_steps) {
+#pragma unroll
+          for (int m = 0; m < K::MT; ++m)
+            a[slot][m] = wb.load(wn_off + m * MSTRIDE + (uint32_t)(sn - STEPS) * 1024u);
+        }
       } else if (sn < STEPS) {
 #pragma unroll
         for (int m = 0; m < K::MT; ++m) a[slot][m] = wl[m][(size_t)sn * 64];
@@ -493,7 +520,14 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
       for (int m = 0; m < K::MT; ++m)
         ring[d][m] = wblk[(size_t)((wave % K::CG) * K::MT + m) * LSTEPS * 64 + (size_t)d * 64 + lane];
   }
+  WBuf wb;
+  wb.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)wpk, (short)0, 0x7fffffff, 0x00020000);
+  wb.voff = lane * 16;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const uint32_t ct0_off = (uint32_t)(STEM + (size_t)((wave_u % K::CG) * K::MT) * LSTEPS * 64) * 16u;
   for (int L = 0; L < n_convs; ++L) {
+    const uint32_t wl_off = ct0_off + (uint32_t)((size_t)L * LAYER * 16u);
+    const uint32_t wn_off = wl_off + (uint32_t)(LAYER * 16u);
     const bf16x8 *wl[K::MT], *wn[K::MT];
 #pragma unroll
     for (int m = 0; m < K::MT; ++m) {
@@ -503,9 +537,9 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
     }
     const int wn_steps = L + 1 < n_convs ? LSTEPS : 0;
     if ((L & 1) == 0)
-      conv_layer<K, KK, DEPTH, false>(X, Y, nb, wl, wn, wn_steps, ring, b, wave, lane);
+      conv_layer<K, KK, DEPTH, false>(X, Y, nb, wl, wn, wn_steps, ring, b, wave, lane, wb, wl_off, wn_off);
     else
-      conv_layer<K, KK, DEPTH, true>(Y, X, nb, wl, wn, wn_steps, ring, b, wave, lane);
+      conv_layer<K, KK, DEPTH, true>(Y, X, nb, wl, wn, wn_steps, ring, b, wave, lane, wb, wl_off, wn_off);
     b += K::C;
     if constexpr (!(K::ABL & 4)) __syncthreads();
   }
@@ -824,7 +858,7 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
 #define ABLATE(X) \
       case 100 + X: return launch<Cfg<128, 256, 7, 6, 2, 4, X>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       ABLATE(0) ABLATE(1) ABLATE(2) ABLATE(4) ABLATE(8) ABLATE(16) ABLATE(24) ABLATE(31) ABLATE(64) ABLATE(128)
-      ABLATE(256) ABLATE(2048)
+      ABLATE(256) ABLATE(2048) ABLATE(32768)
 #undef ABLATE
       case 20: return launch<Cfg<128, 128, 7, 6, 2, 4, 0, 4, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       case 21: return launch<Cfg<128, 128, 7, 6, 4, 4, 0, 4, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
