@@ -152,7 +152,8 @@ class SelfPlayScheduler:
         optim = torch.optim.SGD(self.network.parameters(), weight_decay=0.0001, momentum=0.9, lr=self.lr)
         self.trainer = _Trainer(self.network, optim, memory_size=kw.get("memory_size", 200000),
                                 batch_size=kw.get("batch_size", 64), min_memory=kw.get("min_memory", 20000),
-                                q_average=kw.get("q_average", True), device=self.device)
+                                q_average=kw.get("q_average", True), device=self.device, W=self.W, H=self.H,
+                                A=self.A)
         if resume_model:
             self._load_latest(prev_run=True)
         return self.trainer, None, None
@@ -182,7 +183,9 @@ class SelfPlayScheduler:
             g = D.gather_moves(m, self.W * self.H, self.A) if D.is_distributed() else m
             if g is None:
                 return
-            if update:
+            if update and self.trainer is not None:
+                self.trainer.memory.add_moves(g)  # device replay ring: no per-record host objects
+            elif update:
                 for rec in moves_to_records(g, self.W, self.H):
                     self.memory_queue.put(rec)
             first = {}
@@ -337,14 +340,15 @@ class SelfPlayScheduler:
 
 
 class _Trainer:
-    """UpdateWorker core (updateworker.py:119-149) on the same device: pull, AZ-loss SGD steps, LR on plateau."""
+    """UpdateWorker core (updateworker.py:119-149) on the same device: AZ-loss SGD steps on batches
+    sampled from the device replay ring (replay.DeviceReplay), LR on plateau."""
 
-    def __init__(self, network, optim, memory_size, batch_size, min_memory, q_average, device):
-        from .memory import Memory
+    def __init__(self, network, optim, memory_size, batch_size, min_memory, q_average, device, W=7, H=6, A=7):
+        from .replay import DeviceReplay
 
         self.network = network
         self.optim = optim
-        self.memory = Memory(memory_size)
+        self.memory = DeviceReplay(memory_size, W, H, A, device=device)
         self.batch_size = batch_size
         self.min_memory = min_memory
         self.q_average = q_average
@@ -360,14 +364,11 @@ class _Trainer:
         if len(self.memory) < max(self.batch_size, self.min_memory):
             return None
         self.network.train()
-        batch = self.memory.sample(self.batch_size)
-        s, z, pi, q = Move(*zip(*batch))
-        probs, value = self.network.forward(torch.stack(s).to(self.device))
-        z = torch.stack(z).to(self.device).float()
+        s, z, pi, q = self.memory.sample_batch(self.batch_size)  # mcts.py:234-252 on device tensors
+        probs, value = self.network.forward(s)
         if self.q_average:
-            z = z + torch.stack(q).to(self.device).float()
+            z = z + q
         value_loss = torch.mean((value.view(-1) - z) ** 2)
-        pi = torch.stack(pi).to(self.device).float()
         prob_loss = -(probs.log() * pi).sum() / probs.size(0)
         loss = value_loss + prob_loss
         self.optim.zero_grad()
