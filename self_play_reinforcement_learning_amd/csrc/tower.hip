@@ -560,11 +560,11 @@ __global__ __launch_bounds__(K::THREADS) __attribute__((amdgpu_waves_per_eu(K::W
 // surplus workgroups of the (maximum-size) grid exit at once.
 template <class KF, class KH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_tower_dyn(
-    const __bf16 *planes, const int32_t *count, int cus, int n_blocks, const bf16x8 *wpk, const float *bias,
-    __bf16 *out) {
+    const __bf16 *planes, const int32_t *count, int max_batch, int cus, int n_blocks, const bf16x8 *wpk,
+    const float *bias, __bf16 *out) {
   static_assert(KF::THREADS == 256 && KH::THREADS == 256, "one block size");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int n = *count;
+  const int n = min(*count, max_batch);  // never past the caller's buffers
   const int full_wgs = (n / KF::BOARDS) / cus * cus;
   const int n_full = full_wgs * KF::BOARDS;
   const int rem = n - n_full;
@@ -607,7 +607,7 @@ template <int FF, int CELLS, int A>
 __global__ __launch_bounds__(256) void k_heads(const __bf16 *feats, int n, const int32_t *count, const bf16x8 *wf,
                                                const float *hb, float *probs, float *values) {
   using H = HeadsCfg<FF, CELLS, A>;
-  if (count) n = *count;
+  if (count) n = min(*count, n);  // n = the caller's buffer rows
   const int b0 = blockIdx.x * H::BOARDS;
   if (b0 >= n) return;
   __shared__ __attribute__((aligned(16))) char s_feat[H::BOARDS * H::FS];
@@ -804,8 +804,8 @@ static int launch_dyn(const void *planes, const int32_t *count, int max_batch, i
       return -10;
     attr_set = true;
   }
-  hipLaunchKernelGGL((k_tower_dyn<KF, KH>), dim3(grid), dim3(256), LDS, s, (const __bf16 *)planes, count, cus,
-                     n_blocks, (const bf16x8 *)w, b, (__bf16 *)out);
+  hipLaunchKernelGGL((k_tower_dyn<KF, KH>), dim3(grid), dim3(256), LDS, s, (const __bf16 *)planes, count, max_batch,
+                     cus, n_blocks, (const bf16x8 *)w, b, (__bf16 *)out);
   return hipGetLastError() == hipSuccess ? 0 : -11;
 }
 

@@ -115,6 +115,9 @@ class SelfPlayEngine:
         self.select_timer = None
         self.nn_timer = None
         self.async_device = True  # device-count evaluators run a whole ply without host syncs
+        for ev in (self.evaluator, self.evaluator1):  # outputs sized for every row the arena can emit
+            if ev is not None and hasattr(ev, "reserve"):
+                ev.reserve(self.arena.max_rows, self.device)
         self.refresh_root_prior()
 
     @torch.no_grad()
@@ -190,13 +193,16 @@ class SelfPlayEngine:
     def _dummy_out(self):
         return torch.zeros((1, self.arena.A), dtype=torch.float32, device=self.arena.device)
 
-    def _eval_expand_dev(self):
-        """Network + expand on the device-side row count: no host synchronisation."""
+    def _eval_expand_dev(self, cap=None):
+        """Network + expand on the device-side row count: no host synchronisation.  `cap` bounds the
+        rows (and so the grid): a search step has at most one leaf per game, the end-of-ply
+        expansions up to two."""
         a = self.arena
         if self.nn_timer is not None:
             self.nn_timer.start()
         if self.evaluator1 is None:
-            probs, values = self.evaluator.forward_dev(a.leaves(a.max_rows), a.count_dev, a.max_rows)
+            rows = a.max_rows if cap is None else min(a.max_rows, cap)
+            probs, values = self.evaluator.forward_dev(a.leaves(rows), a.count_dev, rows)
         else:
             probs, values = self.evaluator.forward_dev(a.leaves(a.seg1), a.segment_count_dev(0), a.seg1)
             cap1 = a.max_rows - a.seg1
@@ -217,7 +223,7 @@ class SelfPlayEngine:
         if self._device_count_ok():
             for _ in range(self.iterations):
                 a.select_async(self.select_timer)
-                self._eval_expand_dev()
+                self._eval_expand_dev(cap=self.n_games)
             a.games_end_ply_async()
             self._eval_expand_dev()
         else:

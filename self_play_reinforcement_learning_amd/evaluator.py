@@ -278,6 +278,14 @@ class HipTowerEvaluator(Evaluator):
 
     supports_device_count = True
 
+    def reserve(self, rows, device):
+        """(Re)allocate the device-count path's output buffers for at least `rows` rows."""
+        buf = getattr(self, "_dev_bufs", None)
+        if buf is None or buf[0].shape[0] < rows or buf[0].device != device:
+            self._dev_bufs = (torch.empty((rows, self.cells, self.C // 2), dtype=torch.bfloat16, device=device),
+                              torch.empty((rows, self.A), dtype=torch.float32, device=device),
+                              torch.empty(rows, dtype=torch.float32, device=device))
+
     @torch.no_grad()
     def forward_dev(self, leaves, count_dev, max_rows):
         """Evaluate the first *count_dev rows of `leaves` without a host synchronisation.
@@ -286,13 +294,8 @@ class HipTowerEvaluator(Evaluator):
         count_dev: device int32 holding the row count.  Returns max_rows-row probs/values buffers
         of which the first *count_dev rows are valid (the arena's expand reads the same count)."""
         dev = leaves.device
-        buf = getattr(self, "_dev_bufs", None)
-        if buf is None or buf[0].shape[0] < max_rows or buf[0].device != dev:
-            buf = (torch.empty((max_rows, self.cells, self.C // 2), dtype=torch.bfloat16, device=dev),
-                   torch.empty((max_rows, self.A), dtype=torch.float32, device=dev),
-                   torch.empty(max_rows, dtype=torch.float32, device=dev))
-            self._dev_bufs = buf
-        feats, probs, values = buf
+        self.reserve(max_rows, dev)
+        feats, probs, values = self._dev_bufs
         c = self._lib.ctypes.c_void_p
         stream = c(torch.cuda.current_stream().cuda_stream)
         L = self._lib.lib()
