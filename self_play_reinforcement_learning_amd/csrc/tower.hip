@@ -865,6 +865,8 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
       case 22: return launch<Cfg<128, 128, 7, 6, 2, 4, 0, 2, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       case 23: return launch<Cfg<128, 256, 7, 6, 4, 4, 0, 8>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       case 24: return launch<Cfg<128, 256, 7, 6, 4, 4, 0, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      case 25: return launch<Cfg<128, 256, 7, 6, 2, 4, 0, 8>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      case 26: return launch<Cfg<128, 256, 7, 6, 2, 4, 0, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       default: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
     }
   }
