@@ -226,3 +226,44 @@ def test_compare_models_dropin(tmp_path):
         assert n == 30
         assert total == sum(s["wins"] - s["losses"] for s in breakdown.values())
         assert sum(breakdown["first"].values()) == 15 and sum(breakdown["second"].values()) == 15
+
+
+def test_device_errors_are_raised():
+    """Sticky device error flags surface as SpmctsError: node-pool exhaustion, an illegal
+    play_action, and an exhausted RNG tape (no silent fallbacks)."""
+    from self_play_reinforcement_learning_amd import _lib
+    from self_play_reinforcement_learning_amd.arena import Arena, table_net_eval
+
+    def step(arena, count):
+        if count:
+            p, v = table_net_eval(arena.game, arena.leaves(count), arena.leaf_format, arena.leaf_layout, salt=5)
+            arena.expand(p, v)
+
+    # pool: 4 blocks per tree cannot hold a 25-simulation search
+    a = Arena("connect4", n_trees=4, iterations=25, blocks_per_tree=4, leaf_format="f32")
+    a.tree_reset([0, 1, 2, 3], [1] * 4)
+    a.search_begin([0, 1, 2, 3])
+    for _ in range(25):
+        step(a, a.select())
+    with pytest.raises(_lib.SpmctsError, match="node pool"):
+        a.check()
+    a.close()
+    # illegal action: a full column
+    a = Arena("connect4", n_trees=1, iterations=4, leaf_format="f32")
+    a.tree_reset([0], [1])
+    for _ in range(6):
+        step(a, a.play_action([0], [3]))
+    a.play_action([0], [3])
+    with pytest.raises(_lib.SpmctsError, match="illegal action"):
+        a.check()
+    a.close()
+    # tape: too few recorded doubles for a search
+    a = Arena("connect4", n_trees=1, iterations=8, rng="tape", leaf_format="f32")
+    a.set_tapes([[0.5] * 10])
+    a.tree_reset([0], [1])
+    a.search_begin([0])
+    for _ in range(8):
+        step(a, a.select())
+    with pytest.raises(_lib.SpmctsError, match="tape"):
+        a.check()
+    a.close()

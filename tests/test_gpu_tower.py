@@ -108,3 +108,28 @@ def test_engine_async_matches_sync_path():
         np.testing.assert_array_equal(m1[k], m2[k], err_msg=k)
     for k in ("sims", "moves", "nn_leaves", "terminal_leaves", "depth_sum", "games_finished"):
         assert c1[k] == c2[k], k
+
+
+def test_zero_and_maximum_rows():
+    """Empty batches launch nothing and fail nothing; a device count above the buffer capacity is
+    clamped inside the kernels (no write past the caller's buffers)."""
+    net = _net(7, 6, 7, 2, 32)
+    hip = HipTowerEvaluator(net)
+    x = _planes(7, 6, 64, seed=9).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    p, v = hip(x[:0])
+    assert p.shape[0] == 0 and v.shape[0] == 0
+    cnt = torch.tensor([0], dtype=torch.int32, device=x.device)
+    hip.forward_dev(x, cnt, 64)
+    torch.cuda.synchronize()
+    # count 10,000 into 64-row buffers guarded by 64 extra sentinel rows
+    hip._dev_bufs = None
+    hip.reserve(128, x.device)
+    feats, probs, values = hip._dev_bufs
+    probs.fill_(-7.0)
+    values.fill_(-7.0)
+    cnt.fill_(10_000)
+    hip.forward_dev(x, cnt, 64)
+    torch.cuda.synchronize()
+    assert (probs[64:] == -7.0).all() and (values[64:] == -7.0).all()
+    ref_p, ref_v = hip(x)
+    assert torch.equal(probs[:64], ref_p) and torch.equal(values[:64].view(-1), ref_v.view(-1))
