@@ -1,0 +1,38 @@
+"""Diagnostic: distribution of per-simulation network leaf counts in the bench workload (host-synced path)."""
+import collections
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from self_play_reinforcement_learning_amd.engine import SelfPlayEngine
+from self_play_reinforcement_learning_amd.modules import ResidualTower
+
+plies = int(sys.argv[1]) if len(sys.argv) > 1 else 11
+torch.manual_seed(0)
+net = ResidualTower(7, 6, 7, num_blocks=20, filter_factor=32).cuda().eval()
+eng = SelfPlayEngine("connect4", net, n_games=4096, iterations=200, seed=1234)
+eng.async_device = False
+counts = []
+sel = eng.arena.select
+
+
+def rec(*a, **k):
+    n = sel(*a, **k)
+    counts.append(int(n))
+    return n
+
+
+eng.arena.select = rec
+per_ply = []
+for p in range(plies):
+    k0 = len(counts)
+    eng.ply()
+    c = counts[k0:]
+    per_ply.append(dict(ply=p, min=min(c), max=max(c), mean=sum(c) / len(c),
+                        over_3840=sum(x > 3840 for x in c), n=len(c)))
+    print(json.dumps(per_ply[-1]), flush=True)
+h = collections.Counter((x // 64) * 64 for x in counts)
+print(json.dumps(dict(hist=sorted(h.items()), over_3840=sum(x > 3840 for x in counts), total=len(counts))))

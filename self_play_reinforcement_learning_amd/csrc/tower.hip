@@ -554,15 +554,25 @@ __global__ __launch_bounds__(K::THREADS) __attribute__((amdgpu_waves_per_eu(K::W
   tower_tile<K>(smem, planes, batch, blockIdx.x * K::BOARDS, n_blocks, wpk, bias, out);
 }
 
+// Tail tile for a remainder of `rem` boards after whole rounds of full tiles: the smallest tile
+// (fewest LDS rows, so the shortest workgroup) whose one round of `cus` workgroups covers it.
+// 0 = half (KH), 1 = middle (KM), 2 = full (KF).
+template <class KF, class KM, class KH>
+__host__ __device__ __forceinline__ int tail_kind(int rem, int cus) {
+  if (rem <= cus * KH::BOARDS) return 0;
+  if (rem <= cus * KM::BOARDS) return 1;
+  return 2;
+}
+
 // Device-count driven variant: the batch size is read from device memory (the arena's leaf-row
 // counter), so the host never waits for it.  Workgroups are assigned as in launch_split: whole
-// chip rounds of full-size tiles, then the remainder in half-size tiles when it fits half a round;
-// surplus workgroups of the (maximum-size) grid exit at once.
-template <class KF, class KH>
+// chip rounds of full-size tiles, then the remainder in one round of the smallest tile that covers
+// it (tail_kind); surplus workgroups of the (maximum-size) grid exit at once.
+template <class KF, class KM, class KH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_tower_dyn(
     const __bf16 *planes, const int32_t *count, int max_batch, int cus, int n_blocks, const bf16x8 *wpk,
     const float *bias, __bf16 *out) {
-  static_assert(KF::THREADS == 256 && KH::THREADS == 256, "one block size");
+  static_assert(KF::THREADS == 256 && KM::THREADS == 256 && KH::THREADS == 256, "one block size");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int n = min(*count, max_batch);  // never past the caller's buffers
   const int full_wgs = (n / KF::BOARDS) / cus * cus;
@@ -574,8 +584,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     return;
   }
   const int j = b - full_wgs;
-  if (rem <= cus * KH::BOARDS) {
+  const int kind = tail_kind<KF, KM, KH>(rem, cus);
+  if (kind == 0) {
     if (n_full + j * KH::BOARDS < n) tower_tile<KH>(smem, planes, n, n_full + j * KH::BOARDS, n_blocks, wpk, bias, out);
+  } else if (kind == 1) {
+    if (n_full + j * KM::BOARDS < n) tower_tile<KM>(smem, planes, n, n_full + j * KM::BOARDS, n_blocks, wpk, bias, out);
   } else {
     if (n_full + j * KF::BOARDS < n) tower_tile<KF>(smem, planes, n, n_full + j * KF::BOARDS, n_blocks, wpk, bias, out);
   }
@@ -773,9 +786,10 @@ static int num_cus() {
 }
 
 // Full-size workgroups (one per CU, BOARDS boards each) for whole rounds of the chip, then the
-// remainder with half-size workgroups (half the boards, half the time) when it fits in half a
-// round: a batch of 3,800 boards costs 2.5 workgroup-rounds instead of 3.
-template <class KF, class KH>
+// remainder in one round of the smallest tile that covers it (tail_kind: half-size tiles take about
+// half the time, 4-board tiles three quarters): a batch of 3,700 boards costs 2.5 workgroup-rounds
+// instead of 3, one of 4,096 boards 2.75.
+template <class KF, class KM, class KH>
 static int launch_split(const char *planes, int batch, int n_blocks, const void *w, const float *b, char *out,
                         hipStream_t s) {
   const int cus = num_cus();
@@ -787,25 +801,28 @@ static int launch_split(const char *planes, int batch, int n_blocks, const void 
   if (rc || rem <= 0) return rc;
   const char *p2 = planes + (size_t)n_full * KF::CELLS * 3 * 2;
   char *o2 = out + (size_t)n_full * KF::CELLS * KF::HEAD * 2;
-  if (rem <= cus * KH::BOARDS) return launch<KH>(p2, rem, n_blocks, w, b, o2, s);
-  return launch<KF>(p2, rem, n_blocks, w, b, o2, s);
+  switch (tail_kind<KF, KM, KH>(rem, cus)) {
+    case 0: return launch<KH>(p2, rem, n_blocks, w, b, o2, s);
+    case 1: return launch<KM>(p2, rem, n_blocks, w, b, o2, s);
+    default: return launch<KF>(p2, rem, n_blocks, w, b, o2, s);
+  }
 }
 
-template <class KF, class KH>
+template <class KF, class KM, class KH>
 static int launch_dyn(const void *planes, const int32_t *count, int max_batch, int n_blocks, const void *w,
                       const float *b, void *out, hipStream_t s) {
   const int cus = num_cus();
   const int grid = (max_batch + KF::BOARDS - 1) / KF::BOARDS + cus;
-  constexpr int LDS = KF::LDS > KH::LDS ? KF::LDS : KH::LDS;
+  constexpr int LDS = KF::LDS > KM::LDS ? (KF::LDS > KH::LDS ? KF::LDS : KH::LDS) : (KM::LDS > KH::LDS ? KM::LDS : KH::LDS);
   static bool attr_set = false;
   if (!attr_set) {
-    if (hipFuncSetAttribute((const void *)k_tower_dyn<KF, KH>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS) !=
+    if (hipFuncSetAttribute((const void *)k_tower_dyn<KF, KM, KH>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS) !=
         hipSuccess)
       return -10;
     attr_set = true;
   }
-  hipLaunchKernelGGL((k_tower_dyn<KF, KH>), dim3(grid), dim3(256), LDS, s, (const __bf16 *)planes, count, max_batch,
-                     cus, n_blocks, (const bf16x8 *)w, b, (__bf16 *)out);
+  hipLaunchKernelGGL((k_tower_dyn<KF, KM, KH>), dim3(grid), dim3(256), LDS, s, (const __bf16 *)planes, count,
+                     max_batch, cus, n_blocks, (const bf16x8 *)w, b, (__bf16 *)out);
   return hipGetLastError() == hipSuccess ? 0 : -11;
 }
 
@@ -820,16 +837,16 @@ extern "C" int spmcts_tower_forward_dev(int32_t width, int32_t height, int32_t c
   if (n_blocks < 0 || max_batch < 0 || !count_dev) return -3;
   if (max_batch == 0) return 0;
   if (width == 7 && height == 6 && channels == 128)
-    return launch_dyn<Cfg<128, 256, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(planes_dev, count_dev, max_batch, n_blocks,
+    return launch_dyn<Cfg<128, 256, 7, 6, 2>, Cfg<128, 192, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(planes_dev, count_dev, max_batch, n_blocks,
                                                                       weights_dev, bias_dev, features_dev, s);
   if (width == 7 && height == 6 && channels == 256)
-    return launch_dyn<Cfg<256, 128, 7, 6, 4>, Cfg<256, 128, 7, 6, 4>>(planes_dev, count_dev, max_batch, n_blocks,
+    return launch_dyn<Cfg<256, 128, 7, 6, 4>, Cfg<256, 128, 7, 6, 4>, Cfg<256, 128, 7, 6, 4>>(planes_dev, count_dev, max_batch, n_blocks,
                                                                       weights_dev, bias_dev, features_dev, s);
   if (width == 3 && height == 3 && channels == 128)
-    return launch_dyn<Cfg<128, 256, 3, 3, 2>, Cfg<128, 128, 3, 3, 2>>(planes_dev, count_dev, max_batch, n_blocks,
+    return launch_dyn<Cfg<128, 256, 3, 3, 2>, Cfg<128, 192, 3, 3, 2>, Cfg<128, 128, 3, 3, 2>>(planes_dev, count_dev, max_batch, n_blocks,
                                                                       weights_dev, bias_dev, features_dev, s);
   if (width == 3 && height == 3 && channels == 256)
-    return launch_dyn<Cfg<256, 128, 3, 3, 4>, Cfg<256, 128, 3, 3, 4>>(planes_dev, count_dev, max_batch, n_blocks,
+    return launch_dyn<Cfg<256, 128, 3, 3, 4>, Cfg<256, 128, 3, 3, 4>, Cfg<256, 128, 3, 3, 4>>(planes_dev, count_dev, max_batch, n_blocks,
                                                                       weights_dev, bias_dev, features_dev, s);
   return -2;
 }
@@ -851,10 +868,10 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
     switch (cg) {
       case 1: return launch<Cfg<128, 256, 7, 6, 1>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       case 4: return launch<Cfg<128, 256, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-      case 3: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      case 3: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 128, 7, 6, 4>, Cfg<128, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       case 5: return launch<Cfg<128, 256, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-      case 8: return launch_split<Cfg<128, 256, 7, 6, 2, 8>, Cfg<128, 128, 7, 6, 2, 8>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-      case 9: return launch_split<Cfg<128, 256, 7, 6, 4, 8>, Cfg<128, 128, 7, 6, 4, 8>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      case 8: return launch_split<Cfg<128, 256, 7, 6, 2, 8>, Cfg<128, 128, 7, 6, 2, 8>, Cfg<128, 128, 7, 6, 2, 8>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      case 9: return launch_split<Cfg<128, 256, 7, 6, 4, 8>, Cfg<128, 128, 7, 6, 4, 8>, Cfg<128, 128, 7, 6, 4, 8>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
 #define ABLATE(X) \
       case 100 + X: return launch<Cfg<128, 256, 7, 6, 2, 4, X>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       ABLATE(0) ABLATE(1) ABLATE(2) ABLATE(4) ABLATE(8) ABLATE(16) ABLATE(24) ABLATE(31) ABLATE(64) ABLATE(128)
@@ -867,7 +884,8 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
       case 24: return launch<Cfg<128, 256, 7, 6, 4, 4, 0, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       case 25: return launch<Cfg<128, 256, 7, 6, 2, 4, 0, 8>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       case 26: return launch<Cfg<128, 256, 7, 6, 2, 4, 0, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-      default: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      case 10: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);  // two tile sizes only
+      default: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 192, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
     }
   }
   if (width == 7 && height == 6 && channels == 256)
