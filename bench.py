@@ -10,7 +10,9 @@ A *step* is one ply of every game slot of every rank: 200 PUCT simulations
 env step and tree reuse (engine.SelfPlayEngine.ply).  Finished games are
 refilled immediately (steady state); after every ply the episode statistics
 are all-reduced over ranks and finished games' Move records are gathered to
-rank 0 (the replay owner), as in the north star.
+rank 0 (the replay owner), as in the north star.  Each GPU's games are held in
+--lanes arenas (default 2, engine.LanedEngine) on their own HIP streams, so one
+arena's tree kernels run beside the other's ResNet launch.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
@@ -131,6 +133,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="skip the rank-0 Move gather")
     ap.add_argument("--mode", choices=["selfplay", "arena"], default="selfplay")
+    ap.add_argument("--lanes", type=int, default=2,
+                    help="arenas per GPU on their own HIP streams (engine.LanedEngine); 1 = one arena")
     args = ap.parse_args()
     arena_mode = args.mode == "arena"
 
@@ -144,7 +148,7 @@ def main():
     import torch
 
     from self_play_reinforcement_learning_amd import distributed as D
-    from self_play_reinforcement_learning_amd.engine import SelfPlayEngine
+    from self_play_reinforcement_learning_amd.engine import LanedEngine, SelfPlayEngine, union_ms
     from self_play_reinforcement_learning_amd.modules import ResidualTower
 
     rank, world, local = D.init_from_env()
@@ -157,9 +161,12 @@ def main():
     if arena_mode:  # BASELINE config 5: two frozen nets, greedy (evaluate-mode) MCTS on both sides
         torch.manual_seed(1)
         opponent = ResidualTower(7, 6, 7, num_blocks=args.blocks, filter_factor=args.filter_factor).to(dev).eval()
-    eng = SelfPlayEngine("connect4", net, n_games=args.games, iterations=args.sims, seed=1234 + rank,
-                         device=dev, bucket=args.bucket, opponent=opponent, evaluate=arena_mode,
-                         record=not arena_mode)
+    kw = dict(iterations=args.sims, seed=1234 + rank, device=dev, bucket=args.bucket, opponent=opponent,
+              evaluate=arena_mode, record=not arena_mode)
+    if args.lanes > 1:
+        eng = LanedEngine("connect4", net, n_games=args.games, lanes=args.lanes, **kw)
+    else:
+        eng = SelfPlayEngine("connect4", net, n_games=args.games, **kw)
     gathered = []
 
     def on_moves(m):
@@ -182,6 +189,8 @@ def main():
 
     D.barrier()
     torch.cuda.synchronize()
+    ref = torch.cuda.Event(enable_timing=True)  # time origin of the launch intervals (all lanes' streams)
+    ref.record()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         one_step()
@@ -206,15 +215,22 @@ def main():
     bytes_per_launch = sel_bytes / max(1, sel_launches)
     achieved = bytes_per_launch / sel_avg_s / 1e9 if sel_avg_s > 0 else 0.0
 
-    # ---- network (MFMA) share
-    nn_ms = eng.nn_timer.total_ms()
+    # ---- network (MFMA) share: busy time = union of the network launches of all lanes
+    nn_ms = union_ms(eng.nn_timer.intervals(ref))
     rows = c1["nn_leaves"] - c0["nn_leaves"]
     fpl = resnet_flops_per_leaf(7, 6, 7, args.filter_factor, args.blocks)
     nn_tflops = rows * fpl / (nn_ms / 1e3) / 1e12 if nn_ms > 0 else 0.0
-    # ---- dominant kernel: k_tower (HIP events around each tower launch on the arena's stream)
+    # ---- dominant kernel: k_tower (HIP events around each tower dispatch on its lane's stream).
+    # With L lanes the L dispatches of one simulation step run concurrently on the chip, so a
+    # "launch" here is that group of L dispatches and its duration is their busy (union) time; at
+    # L = 1 this is exactly the per-dispatch average.  The per-dispatch average (what rocprof's
+    # kernel stats report) is kept beside it as avg_dispatch_us.
     tw = eng.tower_timer
-    tw_ms = tw.total_ms() if tw is not None and tw.count() else 0.0
-    tw_launches = tw.count() if tw is not None else 0
+    tw_dispatches = tw.count() if tw is not None else 0
+    tw_sum_ms = tw.total_ms() if tw_dispatches else 0.0
+    tw_ms = union_ms(tw.intervals(ref)) if tw_dispatches else 0.0
+    lanes = max(1, args.lanes)
+    tw_launches = tw_dispatches // lanes
     trunk_fpl = fpl - head_linear_flops(7, 6, 7, args.filter_factor)
     tw_flops_per_launch = rows * trunk_fpl / max(1, tw_launches)
     tw_avg_s = tw_ms / 1e3 / max(1, tw_launches)
@@ -225,7 +241,9 @@ def main():
     traffic, traffic_src = None, None
     if os.path.exists(TRAFFIC_FILE) and (args.games, args.sims, args.filter_factor, args.blocks) == (4096, 200, 32, 20):
         with open(TRAFFIC_FILE) as f:
-            traffic = json.load(f)["bytes_per_launch"]
+            tj = json.load(f)
+        # per-dispatch bytes x dispatches per launch (a launch = one simulation step over all lanes)
+        traffic = tj.get("bytes_per_dispatch", tj["bytes_per_launch"]) * max(1, args.lanes)
         traffic_src = os.path.relpath(TRAFFIC_FILE, HERE)
 
     out = {
@@ -249,6 +267,7 @@ def main():
             "sims_per_move": args.sims,
             "net": f"ResidualTower(filter_factor={args.filter_factor}, num_blocks={args.blocks})",
             "parallelism": f"dp{world}",
+            "lanes_per_gpu": max(1, args.lanes),
         },
         "roofline": {
             "kernel": f"tower::k_tower_dyn (fused ResNet-{4 * args.filter_factor}x{args.blocks} trunk, bf16 MFMA)",
@@ -264,6 +283,11 @@ def main():
             "flops_per_leaf": trunk_fpl,
             "avg_launch_us": tw_avg_s * 1e6,
             "launches": tw_launches,
+            "lanes": lanes,
+            "launch_def": (f"one simulation step = {lanes} concurrent k_tower_dyn dispatches (one per lane stream); "
+                           "duration = their union busy time" if lanes > 1 else "one k_tower_dyn dispatch"),
+            "avg_dispatch_us": tw_sum_ms / max(1, tw_dispatches) * 1e3,
+            "dispatches": tw_dispatches,
         },
         "tree_roofline": {
             "kernel": "k_select<C4> (PUCT tree walk)",

@@ -4,11 +4,12 @@
 set -u
 mkdir -p gpurun_out/prof
 export TMPDIR=/tmp
-ARGS="--steps ${PSTEPS:-3} --warmup 1 --no-cpu-baseline"
+ARGS="--steps ${PSTEPS:-3} --warmup 1 --no-cpu-baseline --lanes ${LANES:-2}"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof/trace -o run -- \
   python3 bench.py $ARGS > gpurun_out/prof/bench_traced.json 2> gpurun_out/prof/trace.err
 rc=$?; echo "trace rc=$rc"; cut -c1-300 gpurun_out/prof/bench_traced.json
 if [ $rc -ne 0 ]; then tail -5 gpurun_out/prof/trace.err; exit $rc; fi
+python3 scripts/tower_union.py gpurun_out/prof/trace/run_kernel_trace.csv ${LANES:-2} gpurun_out/prof/k_tower_union.json
 i=0
 for set in "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
@@ -18,4 +19,4 @@ for set in "FETCH_SIZE" "WRITE_SIZE"; do
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/prof/pmc$i.err; exit $rc; fi
 done
 python3 scripts/pmc_traffic.py gpurun_out/prof/pmc1/run_counter_collection.csv \
-  gpurun_out/prof/pmc2/run_counter_collection.csv gpurun_out/prof/k_tower_traffic.json
+  gpurun_out/prof/pmc2/run_counter_collection.csv gpurun_out/prof/k_tower_traffic.json ${LANES:-2}

@@ -1,0 +1,64 @@
+"""Prototype: two half-size arenas on two HIP streams, simulations interleaved (overlap of one
+lane's tree kernels with the other lane's tower), vs one 4096-game arena."""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from self_play_reinforcement_learning_amd.engine import SelfPlayEngine
+from self_play_reinforcement_learning_amd.modules import ResidualTower
+
+G = int(os.environ.get("GAMES", 4096))
+LANES = int(os.environ.get("LANES", 2))
+WARM, STEPS = 3, 8
+torch.manual_seed(0)
+net = ResidualTower(7, 6, 7, num_blocks=20, filter_factor=32).cuda().eval()
+
+
+def ply_lanes(engs, streams):
+    for e, s in zip(engs, streams):
+        with torch.cuda.stream(s):
+            if not e.started:
+                e.start()
+            e.arena.games_begin_ply()
+    for _ in range(engs[0].iterations):
+        for e, s in zip(engs, streams):
+            with torch.cuda.stream(s):
+                e.arena.select_async()
+                e._eval_expand_dev(cap=e.n_games)
+    for e, s in zip(engs, streams):
+        with torch.cuda.stream(s):
+            e.arena.games_end_ply_async()
+            e._eval_expand_dev()
+    for e, s in zip(engs, streams):
+        with torch.cuda.stream(s):
+            fin, ring = e.arena.games_finish_ply(refill=True)
+            if ring:
+                e.arena.export_moves(ring)
+
+
+res = {}
+for lanes in (1, LANES):
+    n = G // lanes
+    engs = [SelfPlayEngine("connect4", net, n_games=n, iterations=200, seed=1234 + i, subsequence0=i * 2 * n)
+            for i in range(lanes)]
+    streams = [torch.cuda.Stream() for _ in range(lanes)]
+    for _ in range(WARM):
+        ply_lanes(engs, streams)
+    torch.cuda.synchronize()
+    m0 = sum(e.counters()["moves"] for e in engs)
+    t0 = time.perf_counter()
+    for _ in range(STEPS):
+        ply_lanes(engs, streams)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    m1 = sum(e.counters()["moves"] for e in engs)
+    for e in engs:
+        e.check()
+    res[lanes] = dict(positions_per_s=(m1 - m0) / dt, ms_per_ply=dt / STEPS * 1e3)
+    print(json.dumps({"lanes": lanes, **res[lanes]}), flush=True)
+    del engs
+    torch.cuda.empty_cache()

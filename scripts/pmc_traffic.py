@@ -15,17 +15,21 @@ def mean_counter(path, name, kernel="k_tower_dyn"):
     return sum(vals) / len(vals), len(vals)
 
 
-def main(fetch_csv, write_csv, out_json):
+def main(fetch_csv, write_csv, out_json, lanes="1"):
+    lanes = int(lanes)
     fetch, n = mean_counter(fetch_csv, "FETCH_SIZE")
     write, _ = mean_counter(write_csv, "WRITE_SIZE")
-    res = dict(kernel="k_tower_dyn", launches=n, fetch_kib=fetch, write_kib=write,
+    per_dispatch = 2 * fetch * 1024 + write * 1024
+    res = dict(kernel="k_tower_dyn", dispatches=n, lanes=lanes, fetch_kib=fetch, write_kib=write,
                read_bytes=2 * fetch * 1024, write_bytes=write * 1024,
-               bytes_per_launch=2 * fetch * 1024 + write * 1024,
-               note="FETCH_SIZE x2 (gfx950 16-B read correction) + WRITE_SIZE, KiB -> bytes; "
-                    "L2<->fabric traffic (Infinity Cache hits included)")
+               bytes_per_dispatch=per_dispatch,
+               bytes_per_launch=per_dispatch * lanes,
+               note="per dispatch: FETCH_SIZE x2 (gfx950 16-B read correction) + WRITE_SIZE, KiB -> bytes; "
+                    "L2<->fabric traffic (Infinity Cache hits included); a launch = `lanes` concurrent "
+                    "dispatches (bench.py roofline)")
     json.dump(res, open(out_json, "w"), indent=1)
     print(json.dumps(res))
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])

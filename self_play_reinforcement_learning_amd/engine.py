@@ -61,6 +61,26 @@ class EventTimer:
     def count(self):
         return len(self.pairs)
 
+    def intervals(self, ref):
+        """[(start_ms, end_ms)] of every recorded pair relative to the event `ref` (any stream)."""
+        torch.cuda.synchronize()
+        return [(ref.elapsed_time(a), ref.elapsed_time(b)) for a, b in self.pairs if b is not None]
+
+
+def union_ms(intervals):
+    """Length of the union of [start, end) intervals (ms): busy time of possibly overlapping launches."""
+    total, cur_s, cur_e = 0.0, None, None
+    for a, b in sorted(intervals):
+        if cur_e is None or a > cur_e:
+            if cur_e is not None:
+                total += cur_e - cur_s
+            cur_s, cur_e = a, b
+        else:
+            cur_e = max(cur_e, b)
+    if cur_e is not None:
+        total += cur_e - cur_s
+    return total
+
 
 class SelfPlayEngine:
     def __init__(self, game, network, n_games=4096, iterations=200, alpha=1.0, strong_play=False, evaluate=False,
@@ -214,26 +234,43 @@ class SelfPlayEngine:
         else:
             a.expand2(probs, values, p1, v1)
 
-    def ply(self, on_moves=None, refill=True):
-        """Advance every active game by one move. Returns (#games finished, #records exported)."""
+    # --- one ply in phases (LanedEngine interleaves the phases of several engines on their streams)
+    def _ply_begin(self):
         if not self.started:
             self.start()
+        self.arena.games_begin_ply()
+
+    def _ply_simulation(self):
+        """One lock-step simulation of every searching tree, without a host synchronisation."""
+        self.arena.select_async(self.select_timer)
+        self._eval_expand_dev(cap=self.n_games)
+
+    def _ply_move(self):
+        self.arena.games_end_ply_async()
+        self._eval_expand_dev()
+
+    def ply(self, on_moves=None, refill=True):
+        """Advance every active game by one move. Returns (#games finished, #records exported)."""
+        self._ply_begin()
         a = self.arena
-        a.games_begin_ply()
         if self._device_count_ok():
             for _ in range(self.iterations):
-                a.select_async(self.select_timer)
-                self._eval_expand_dev(cap=self.n_games)
-            a.games_end_ply_async()
-            self._eval_expand_dev()
+                self._ply_simulation()
+            self._ply_move()
         else:
             for _ in range(self.iterations):
                 self._eval_expand(a.select(self.select_timer))
             self._eval_expand(a.games_end_ply())
+        return self._ply_finish(on_moves, refill)
+
+    def _ply_finish(self, on_moves=None, refill=True, game_offset=0):
+        a = self.arena
         finished, ring = a.games_finish_ply(refill=refill)
         exported = 0
         if ring:
             moves = a.export_moves(ring)
+            if game_offset:
+                moves["game"] += game_offset
             exported = int(moves["z"].shape[0])
             if on_moves is not None:
                 on_moves(moves)
@@ -273,6 +310,18 @@ class SelfPlayEngine:
         swap_sides alternates across calls exactly as the reference's task ids do.
         Under torch.distributed every rank plays its own `n` and keeps stepping (idle plies)
         until all ranks are done, so the per-ply collectives in on_moves / on_ply stay matched."""
+        target = self._play_games_setup(n)
+        plies = 0
+        while not distributed.all_ranks_true(self.games_done >= target):
+            self.ply(on_moves=on_moves)
+            plies += 1
+            if on_ply is not None:
+                on_ply(self)
+        self._started = self._limit
+        return plies
+
+    def _play_games_setup(self, n):
+        """Raise the game budget by `n` and start idle slots; returns the games_done target."""
         a = self.arena
         started = getattr(self, "_started", 0)
         limit = started + max(0, n)
@@ -284,15 +333,8 @@ class SelfPlayEngine:
             if k:
                 a.games_start(idle[:k])
             self.started = True
-        target = self.games_done + max(0, n)
-        plies = 0
-        while not distributed.all_ranks_true(self.games_done >= target):
-            self.ply(on_moves=on_moves)
-            plies += 1
-            if on_ply is not None:
-                on_ply(self)
-        self._started = limit
-        return plies
+        self._limit = limit
+        return self.games_done + max(0, n)
 
     def counters(self):
         return self.arena.counters()
@@ -305,3 +347,163 @@ class SelfPlayEngine:
 
     def check(self):
         self.arena.check()
+
+
+class _SumTimer:
+    """The per-lane EventTimers of one kind seen as one (sums; launches of all lanes)."""
+
+    def __init__(self, timers):
+        self.timers = timers
+
+    def total_ms(self):
+        return sum(t.total_ms() for t in self.timers)
+
+    def count(self):
+        return sum(t.count() for t in self.timers)
+
+    def intervals(self, ref):
+        return [iv for t in self.timers for iv in t.intervals(ref)]
+
+
+class LanedEngine:
+    """`lanes` SelfPlayEngines of n_games / lanes slots each, on their own HIP streams, stepped in
+    lock step: every simulation issues each lane's select -> tower -> heads -> expand on that lane's
+    stream, so one lane's tree kernels (and the tail workgroups of its tower launch) run beside the
+    other lane's tower launch instead of leaving the chip idle between dependent launches.
+
+    Same public surface as SelfPlayEngine (ply / run / play_games / counters / stats_vector / check /
+    enable_timers / refresh_network).  Lane i uses the Philox subsequences of trees
+    [offset_i, offset_i + 2 n_i) of a single arena of n_games slots (same seed), and its exported
+    game ids are offset by i * 2**40 (even, so swap_sides = id odd is preserved and ids stay unique).
+    Each lane is a complete arena: results are those of `lanes` independent engines."""
+
+    GAME_ID_STRIDE = 1 << 40
+
+    def __init__(self, game, network, n_games=4096, lanes=2, seed=0, subsequence0=None, device=None, **kw):
+        if lanes < 1 or n_games < lanes:
+            raise ValueError(f"need 1 <= lanes <= n_games (lanes={lanes}, n_games={n_games})")
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        rank = distributed.env_rank()[0]
+        if subsequence0 is None:
+            subsequence0 = rank * 2 * n_games
+        sizes = [n_games // lanes + (1 if i < n_games % lanes else 0) for i in range(lanes)]
+        self.streams = [torch.cuda.Stream(device=self.device) for _ in range(lanes)]
+        self.lanes = []
+        off = 0
+        for i, (n, st) in enumerate(zip(sizes, self.streams)):
+            with torch.cuda.stream(st):
+                self.lanes.append(SelfPlayEngine(game, network, n_games=n, seed=seed, subsequence0=subsequence0 + 2 * off,
+                                                 device=self.device, **kw))
+            off += n
+        torch.cuda.synchronize(self.device)
+        self.n_games = n_games
+        self.iterations = self.lanes[0].iterations
+        self.evaluator = self.lanes[0].evaluator
+        self.select_timer = self.nn_timer = self.tower_timer = None
+
+    def _each(self, fn):
+        out = []
+        for e, st in zip(self.lanes, self.streams):
+            with torch.cuda.stream(st):
+                out.append(fn(e))
+        return out
+
+    @property
+    def positions(self):
+        return sum(e.positions for e in self.lanes)
+
+    @property
+    def games_done(self):
+        return sum(e.games_done for e in self.lanes)
+
+    @property
+    def started(self):
+        return all(e.started for e in self.lanes)
+
+    def start(self):
+        self._each(lambda e: e.start())
+
+    def enable_timers(self, on=True):
+        self._each(lambda e: e.enable_timers(on))
+        if on:
+            self.select_timer = _SumTimer([e.select_timer for e in self.lanes])
+            self.nn_timer = _SumTimer([e.nn_timer for e in self.lanes])
+            self.tower_timer = _SumTimer([e.tower_timer for e in self.lanes])
+        else:
+            self.select_timer = self.nn_timer = self.tower_timer = None
+
+    def refresh_network(self):
+        self._each(lambda e: e.refresh_network())
+
+    def ply(self, on_moves=None, refill=True):
+        """One move of every active game of every lane. Returns (#games finished, #records exported)."""
+        if not all(e._device_count_ok() for e in self.lanes):
+            res = [(e.ply(on_moves, refill)) for e in self.lanes]
+        else:
+            self._each(lambda e: e._ply_begin())
+            for _ in range(self.iterations):
+                self._each(lambda e: e._ply_simulation())
+            self._each(lambda e: e._ply_move())
+            res = []
+            for i, (e, st) in enumerate(zip(self.lanes, self.streams)):
+                with torch.cuda.stream(st):  # on_moves runs on the lane's stream, after its export
+                    res.append(e._ply_finish(on_moves, refill, game_offset=i * self.GAME_ID_STRIDE))
+        for st in self.streams:  # later work on the caller's stream sees every lane's ply
+            if st is not None:
+                torch.cuda.current_stream(self.device).wait_stream(st)
+        return sum(r[0] for r in res), sum(r[1] for r in res)
+
+    def run(self, plies=None, games=None, seconds=None, on_moves=None):
+        t0 = time.time()
+        n = 0
+        while True:
+            self.ply(on_moves=on_moves)
+            n += 1
+            if plies is not None and n >= plies:
+                break
+            if games is not None and self.games_done >= games:
+                break
+            if seconds is not None and time.time() - t0 >= seconds:
+                break
+        return dict(plies=n, seconds=time.time() - t0, games=self.games_done, positions=self.positions)
+
+    def play_games(self, n, on_moves=None, on_ply=None):
+        """As SelfPlayEngine.play_games, the n games split over the lanes."""
+        k = len(self.lanes)
+        parts = [n // k + (1 if i < n % k else 0) for i in range(k)]
+        targets = []
+        for e, st, m in zip(self.lanes, self.streams, parts):
+            with torch.cuda.stream(st):
+                targets.append(e._play_games_setup(m))
+        plies = 0
+        while not distributed.all_ranks_true(all(e.games_done >= t for e, t in zip(self.lanes, targets))):
+            self.ply(on_moves=on_moves)
+            plies += 1
+            if on_ply is not None:
+                on_ply(self)
+        for e in self.lanes:
+            e._started = e._limit
+        return plies
+
+    def counters(self):
+        cs = self._each(lambda e: e.counters())
+        out = {}
+        for k, v in cs[0].items():
+            if k == "results":
+                out[k] = [[sum(c[k][i][j] for c in cs) for j in range(3)] for i in range(2)]
+            elif k == "blocks_in_use_max":
+                out[k] = max(c[k] for c in cs)
+            elif k == "error_flags":
+                out[k] = 0
+                for c in cs:
+                    out[k] |= c[k]
+            else:
+                out[k] = sum(c[k] for c in cs)
+        return out
+
+    def stats_vector(self):
+        vs = self._each(lambda e: e.stats_vector())
+        return [sum(x) for x in zip(*vs)]
+
+    def check(self):
+        self._each(lambda e: e.check())

@@ -77,6 +77,11 @@ class _FakeEngine:
         self.games_done += self.rate
         on_moves(_moves(0, 0))
 
+    def _play_games_setup(self, n):
+        from self_play_reinforcement_learning_amd.engine import SelfPlayEngine
+
+        return SelfPlayEngine._play_games_setup(self, n)
+
 
 def _loop_worker(rank, world, port, q):
     from self_play_reinforcement_learning_amd.engine import SelfPlayEngine
@@ -109,6 +114,76 @@ def test_play_games_keeps_ranks_in_step_gloo():
     (r0, p0, d0, g0), (r1, p1, d1, g1) = res
     assert p0 == p1 == 6 and g0 == g1 == 6  # rank 0 needs 6 plies for its 6 games; rank 1 idles along
     assert d0 == 6 and d1 == 12
+
+
+class _FakeLane(_FakeEngine):
+    """A LanedEngine lane: the phase methods of SelfPlayEngine.ply; finishes `rate` games per ply."""
+
+    iterations = 3
+
+    def _device_count_ok(self):
+        return True
+
+    def _ply_begin(self):
+        self.sims = 0
+
+    def _ply_simulation(self):
+        self.sims += 1
+
+    def _ply_move(self):
+        assert self.sims == self.iterations
+
+    def _ply_finish(self, on_moves=None, refill=True, game_offset=0):
+        self.plies_run += 1
+        self.games_done += self.rate
+        m = _moves(0, 1)
+        m["game"] += game_offset
+        on_moves(m)
+        return self.rate, 1
+
+
+def _laned_worker(rank, world, port, q):
+    from self_play_reinforcement_learning_amd.engine import LanedEngine
+
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    D.init_from_env(backend="gloo")
+    eng = LanedEngine.__new__(LanedEngine)  # lanes without a GPU: no streams, fake arenas
+    eng.lanes = [_FakeLane(rate=rank + 1), _FakeLane(rate=1)]
+    eng.streams = [None, None]
+    eng.iterations = 3
+    eng.device = torch.device("cpu")
+    games = []
+
+    def on_moves(m):
+        games.append(int(m["game"][0]))
+        D.gather_moves(m, 42, 7)
+
+    plies = eng.play_games(8, on_moves=on_moves, on_ply=lambda e: D.all_reduce_stats([e.games_done]))
+    q.put((rank, plies, [ln.games_done for ln in eng.lanes], games[:2]))
+    torch.distributed.destroy_process_group()
+
+
+def test_laned_engine_play_games_gloo():
+    """LanedEngine splits the games over its lanes, every lane steps every ply (so the per-lane
+    collectives in on_moves match across ranks), and lane i's game ids carry the i * 2**40 offset."""
+    from self_play_reinforcement_learning_amd.engine import LanedEngine
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_laned_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in procs], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, p0, d0, g0), (_, p1, d1, g1) = res
+    # 8 games = 4 per lane; the slowest lane (rate 1) needs 4 plies on both ranks
+    assert p0 == p1 == 4
+    assert d0 == [4, 4] and d1 == [8, 4]
+    assert g0 == [0, LanedEngine.GAME_ID_STRIDE] and g1 == g0
 
 
 def test_pack_unpack_roundtrip():

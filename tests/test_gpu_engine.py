@@ -116,8 +116,10 @@ def test_mcts_facade_with_resnet_plays_full_game():
     assert len(q) > 0 and all(m.state.shape == (7, 6) for m in q)
 
 
-def test_scheduler_train_model_dropin(tmp_path):
-    """run_self_play_connect4.py-style use (stale env_gen=/self_play= kwargs) trains and checkpoints."""
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_scheduler_train_model_dropin(tmp_path, lanes):
+    """run_self_play_connect4.py-style use (stale env_gen=/self_play= kwargs) trains and checkpoints,
+    with one arena or two lanes (LanedEngine)."""
     from self_play_reinforcement_learning_amd import (Connect4Env, MCTreeSearch, ModelContainer, ResidualTower,
                                                       SelfPlayScheduler)
 
@@ -128,8 +130,9 @@ def test_scheduler_train_model_dropin(tmp_path):
     sp = SelfPlayScheduler(env=Connect4Env, network=network, policy_container=container,
                            evaluation_policy_container=None, initial_games=16, epoch_length=24, evaluation_games=0,
                            save_dir=str(tmp_path), self_play=True, stagger=True, stagger_mem_step=100, lr=0.005,
-                           n_games=16)
+                           n_games=16, lanes=lanes)
     sp.train_model(2)
+    assert len(getattr(sp.engine, "lanes", [sp.engine])) == lanes
     saves = sorted(p for p in (tmp_path / sp.start_time).iterdir() if p.name.startswith("model-"))
     assert len(saves) == 2
     ck = torch.load(saves[-1], weights_only=True)
@@ -267,3 +270,42 @@ def test_device_errors_are_raised():
     with pytest.raises(_lib.SpmctsError, match="tape"):
         a.check()
     a.close()
+
+
+def test_laned_engine_plays_like_its_lanes():
+    """LanedEngine = independent lane arenas on their own streams: per-lane results equal those of a
+    SelfPlayEngine with the same slots, seed and Philox subsequences, counters add up, and exported
+    game ids are unique with the swap_sides parity preserved."""
+    import numpy as np
+
+    from self_play_reinforcement_learning_amd.engine import LanedEngine, SelfPlayEngine
+    from self_play_reinforcement_learning_amd.modules import ResidualTower
+
+    torch.manual_seed(0)
+    net = ResidualTower(7, 6, 7, num_blocks=1, filter_factor=32).cuda().eval()
+    laned = LanedEngine("connect4", net, n_games=40, lanes=2, iterations=12, seed=3)
+    got = []
+    laned.run(plies=30, on_moves=lambda m: got.append({k: v.cpu().numpy() for k, v in m.items()}))
+    laned.check()
+    # lane 1 alone: 20 slots, trees 40..79 of the 40-game arena's Philox subsequences
+    solo = SelfPlayEngine("connect4", net, n_games=20, iterations=12, seed=3, subsequence0=40)
+    ref = []
+    solo.run(plies=30, on_moves=lambda m: ref.append({k: v.cpu().numpy() for k, v in m.items()}))
+    lane1 = [g for g in got if len(g["game"]) and g["game"][0] >= LanedEngine.GAME_ID_STRIDE]
+    a = {k: np.concatenate([g[k] for g in lane1]) for k in lane1[0]}
+    b = {k: np.concatenate([g[k] for g in ref]) for k in ref[0]}
+    b["game"] = b["game"] + LanedEngine.GAME_ID_STRIDE
+    for k in b:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    c = laned.counters()
+    c0, c1 = laned.lanes[0].counters(), laned.lanes[1].counters()
+    for k in ("sims", "moves", "nn_leaves", "games_finished"):
+        assert c[k] == c0[k] + c1[k], k
+    assert c["moves"] == 30 * 40
+    ids = np.concatenate([g["game"] for g in got])
+    firsts = {}
+    for g in got:  # each game's records come in one batch: the policy's moves, then the opponent's
+        for gid in np.unique(g["game"]):
+            assert gid not in firsts
+            firsts[gid] = True
+    assert len(firsts) == c["games_finished"] and (ids >= 0).all()
