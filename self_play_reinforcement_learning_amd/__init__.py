@@ -9,7 +9,7 @@ Public API mirrors the reference:
     ResidualTower                         (games/general/modules.py)
     Connect4Env, TicTacToeEnv             (games/connect4, games/tictactoe)
     OneStepLookahead, Random              (games/general/hardcoded_players.py)
-plus the arena itself: Arena, SelfPlayEngine, DeviceTableNet.
+plus the arena itself: Arena, SelfPlayEngine, LanedEngine, DeviceTableNet.
 """
 from .base_model import BasePlayer, ModelContainer, Policy, TrainableModel  # noqa: F401
 from .memory import Memory  # noqa: F401
@@ -18,6 +18,7 @@ from .modules import InferenceTower, ResidualTower  # noqa: F401
 _LAZY = {
     "Arena": ".arena",
     "SelfPlayEngine": ".engine",
+    "LanedEngine": ".engine",
     "DeviceTableNet": ".evaluator",
     "make_evaluator": ".evaluator",
     "MCTreeSearch": ".mcts",
