@@ -22,7 +22,8 @@ container = ModelContainer(policy_gen=MCTreeSearch, policy_kwargs=dict(iteration
 ev = ModelContainer(policy_gen=OneStepLookahead, policy_kwargs=dict(env=Connect4Env))
 with tempfile.TemporaryDirectory() as d:
     sp = SelfPlayScheduler(policy_container=container, env=Connect4Env, network=net, evaluation_policy_container=ev,
-                           initial_games=24, epoch_length=20, evaluation_games=10, save_dir=d, n_games=8)
+                           initial_games=24, epoch_length=20, evaluation_games=10, save_dir=d, n_games=8,
+                           lanes=int(os.environ.get("LANES", 2)))
     sp.train_model(2)
     total, breakdown = sp.compare_models()
 mem = len(sp.trainer.memory) if sp.trainer is not None else -1
