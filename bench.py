@@ -135,6 +135,8 @@ def main():
     ap.add_argument("--mode", choices=["selfplay", "arena"], default="selfplay")
     ap.add_argument("--lanes", type=int, default=2,
                     help="arenas per GPU on their own HIP streams (engine.LanedEngine); 1 = one arena")
+    ap.add_argument("--no-pack", action="store_true",
+                    help="lanes > 1: keep round-aligned tower tiles (no SPMCTS_TOWER_PACK)")
     args = ap.parse_args()
     arena_mode = args.mode == "arena"
 
@@ -164,7 +166,7 @@ def main():
     kw = dict(iterations=args.sims, seed=1234 + rank, device=dev, bucket=args.bucket, opponent=opponent,
               evaluate=arena_mode, record=not arena_mode)
     if args.lanes > 1:
-        eng = LanedEngine("connect4", net, n_games=args.games, lanes=args.lanes, **kw)
+        eng = LanedEngine("connect4", net, n_games=args.games, lanes=args.lanes, pack=not args.no_pack, **kw)
     else:
         eng = SelfPlayEngine("connect4", net, n_games=args.games, **kw)
     gathered = []

@@ -255,10 +255,14 @@ int spmcts_head_epilogue(int32_t hidden, int32_t actions, const void *z_dev, int
                          const float *head_b_dev, float *probs_dev, float *values_dev, spmcts_stream stream);
 int spmcts_tower_supported(int32_t width, int32_t height, int32_t channels);
 /* Device-count variants: the batch size is read from count_dev (e.g. the leaf-row count written by
- * spmcts_select) so no host synchronisation is needed; max_batch bounds the grid. */
+ * spmcts_select) so no host synchronisation is needed; max_batch bounds the grid.
+ * flags: SPMCTS_TOWER_PACK = the launch shares the chip with concurrent launches on other streams
+ * (engine.LanedEngine): every board goes in full-size tiles and only the last few boards in one
+ * smaller tile, instead of whole chip rounds of full tiles plus one round of smaller tiles. */
+#define SPMCTS_TOWER_PACK 1
 int spmcts_tower_forward_dev(int32_t width, int32_t height, int32_t channels, int32_t n_blocks, const void *planes_dev,
                              const int32_t *count_dev, int32_t max_batch, const void *weights_dev,
-                             const float *bias_dev, void *features_dev, spmcts_stream stream);
+                             const float *bias_dev, void *features_dev, int32_t flags, spmcts_stream stream);
 int spmcts_tower_heads_dev(int32_t width, int32_t height, int32_t channels, int32_t actions, const void *features_dev,
                            const int32_t *count_dev, int32_t max_batch, const void *head_w_dev,
                            const float *head_b_dev, float *probs_dev, float *values_dev, spmcts_stream stream);

@@ -13,6 +13,7 @@ LIB_PATH = os.environ.get("SPMCTS_LIB", os.path.join(_HERE, "libspmcts.so"))
 
 CONNECT4, TICTACTOE = 0, 1
 RNG_PHILOX, RNG_TAPE = 0, 1
+TOWER_PACK = 1  # spmcts_tower_forward_dev flags (include/spmcts.h SPMCTS_TOWER_PACK)
 LEAF_F32, LEAF_F16, LEAF_BF16, LEAF_BOARD_I64 = 0, 1, 2, 3
 NCHW, NHWC = 0, 1
 PLAYER_MCTS, PLAYER_RANDOM, PLAYER_LOOKAHEAD = 0, 1, 2
@@ -121,7 +122,7 @@ _SIGS = {
     "spmcts_tower_supported": [_I32, _I32, _I32],
     "spmcts_tower_heads": [_I32, _I32, _I32, _I32, _P, _I32, _P, _P, _P, _P, _P],
     "spmcts_head_epilogue": [_I32, _I32, _P, _I32, _I32, _P, _P, _P, _P],
-    "spmcts_tower_forward_dev": [_I32, _I32, _I32, _I32, _P, _P, _I32, _P, _P, _P, _P],
+    "spmcts_tower_forward_dev": [_I32, _I32, _I32, _I32, _P, _P, _I32, _P, _P, _P, _I32, _P],
     "spmcts_tower_heads_dev": [_I32, _I32, _I32, _I32, _P, _P, _I32, _P, _P, _P, _P, _P],
 }
 

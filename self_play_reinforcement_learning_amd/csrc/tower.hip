@@ -35,7 +35,8 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef short i16x2 __attribute__((ext_vector_type(2)));
 
 
-template <int C_, int ROWS_, int W_, int H_, int CG_ = 2, int WAVES_ = 4, int ABL_ = 0, int DEPTH_ = 4, int OCC_ = 1>
+template <int C_, int ROWS_, int W_, int H_, int CG_ = 2, int WAVES_ = 4, int ABL_ = 0, int DEPTH_ = 4, int OCC_ = 1,
+          bool XMAJ_ = false>
 struct Cfg {
   static constexpr int OCC = OCC_;  // resident workgroups per CU the register budget is sized for
   static constexpr int DEPTH = DEPTH_;  // weight-fragment prefetch distance (k-steps)
@@ -69,6 +70,27 @@ struct Cfg {
   static_assert(CG * MG == WAVES, "wave plan");
   static_assert(BOARDS >= 1, "board larger than a tile");
   static_assert(LDS <= 163840, "LDS budget");
+  // Row layout of the tile.  Board-major (default): row = board * CELLS + x * H + y.  Column-major
+  // across boards (XMAJ): row = x * (BOARDS * H) + board * H + y, so each board column x of all the
+  // tile's boards is BOARDS*H consecutive rows: with 6 boards (36 rows per column) cell tile 0 lies
+  // in column 0 and tile 7 in column 6, whose dx = -1 / +1 taps read only zero padding and are
+  // skipped (conv_layer_x): 6 of the 72 (tile, tap) pairs of the workgroup, 8.3 % of the MFMAs.
+  // A neighbour stays an affine row offset in both layouts: dx * DX + dy.
+  static constexpr bool XMAJ = XMAJ_;
+  static constexpr int DX = XMAJ ? BOARDS * H : H;
+  // (board, x, y) of a row < VROWS
+  __host__ __device__ static constexpr int row_board(int row) { return XMAJ ? (row / H) % BOARDS : row / CELLS; }
+  __host__ __device__ static constexpr int row_x(int row) { return XMAJ ? row / (BOARDS * H) : (row % CELLS) / H; }
+  __host__ __device__ static constexpr int row_y(int row) { return row % H; }
+  __host__ __device__ static constexpr int row_cell(int row) { return row_x(row) * H + row_y(row); }
+  // does any on-board row of 32-row cell tile T have an on-board neighbour column x + dx?
+  __host__ __device__ static constexpr bool tile_dx_live(int T, int dx) {
+    for (int r = T * 32; r < T * 32 + 32 && r < VROWS; ++r) {
+      const int nx = row_x(r) + dx;
+      if (nx >= 0 && nx < W) return true;
+    }
+    return false;
+  }
 };
 
 __device__ __forceinline__ bf16x8 lds_b128(const char *p) { return *(const bf16x8 *)p; }
@@ -106,7 +128,7 @@ struct Nbr {
       rowi[t] = row;
       uint32_t m = 0;
       if (row < K::VROWS) {
-        const int c = row % K::CELLS, x = c / K::H, y = c % K::H;
+        const int x = K::row_x(row), y = K::row_y(row);
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
           const int nx = x + tap / 3 - 1, ny = y + tap % 3 - 1;
@@ -118,8 +140,8 @@ struct Nbr {
   }
   // byte offset of the source row of tile t for `tap` (the zero row when off the board)
   __device__ __forceinline__ int off(int t, int tap) const {
-    const int d = ((tap / 3 - 1) * K::H + (tap % 3 - 1)) * K::RS;
-    const int dr = (tap / 3 - 1) * K::H + (tap % 3 - 1);
+    const int dr = (tap / 3 - 1) * K::DX + (tap % 3 - 1);
+    const int d = dr * K::RS;
     return ((mask[t] >> tap) & 1u) ? base[t] + d : (K::ZROW + ((rowi[t] + dr) & (K::NZ - 1))) * K::RS;
   }
 };
@@ -395,6 +417,135 @@ __device__ __forceinline__ void conv_layer(const char *src, char *dst, const Nbr
   }
 }
 
+// Column-group conv for XMAJ tiles (Cfg::XMAJ).  The 9 taps run as three groups of one board-column
+// offset dx = -1, 0, +1 (taps 3g .. 3g+2); in group g the wave issues the MFMAs and operand reads
+// of only its LIVE cell tiles: a tile all of whose rows lie in board column 0 (dx = -1) or W-1
+// (dx = +1) would multiply zero padding only.  Skipped contributions are exact zeros, so the
+// results equal conv_layer's.  The wave's row half MG_ is a template argument, which makes the
+// live sets compile-time; everything else is conv_layer's pipeline (B one step ahead from LDS,
+// weight ring DEPTH steps ahead and on into the next layer, bias/residual in the epilogue).
+template <class K, int MG_>
+struct XLive {
+  static constexpr uint32_t mask(int g) {
+    uint32_t m = 0;
+    for (int t = 0; t < K::NT; ++t)
+      if (K::tile_dx_live(MG_ * K::NT + t, g - 1)) m |= 1u << t;
+    return m;
+  }
+  static constexpr uint32_t popc(uint32_t m) { return m ? (m & 1u) + popc(m >> 1) : 0u; }
+  static constexpr uint32_t ALL = (1u << K::NT) - 1;
+  static constexpr uint32_t LIVE[3] = {mask(0), mask(1), mask(2)};
+  // tiles not live in group 0 miss the zero-start step 0: their accumulators start at zero
+  static constexpr uint32_t ZPRE = ALL & ~LIVE[0];
+};
+
+template <class K, int KK, int DEPTH, int MG_, int G>
+__device__ __forceinline__ void conv_group_x(const char *src, const Nbr<K> &nb, f32x16 (&acc)[K::MT][K::NT],
+                                             bf16x8 (&bc)[K::NT], bf16x8 (&bn)[K::NT], int (&off_cur)[K::NT],
+                                             int (&off_nxt)[K::NT], bf16x8 (&a)[DEPTH][K::MT], int hoff,
+                                             const WBuf &wb, uint32_t wl_off, uint32_t wn_off, int wn_steps) {
+  using X = XLive<K, MG_>;
+  constexpr uint32_t MSTRIDE = 9u * KK * 1024u;
+  constexpr int STEPS = 9 * KK;
+  constexpr uint32_t LV = X::LIVE[G];
+  constexpr uint32_t LVN = G < 2 ? X::LIVE[G < 2 ? G + 1 : 2] : 0u;  // live tiles of the next group
+  constexpr int NTA = (int)X::popc(LV);
+  static_assert(NTA >= 1 && K::MT * NTA >= NTA + K::MT, "schedule: enough MFMAs for the loads");
+  for (int tap = 3 * G; tap < 3 * G + 3; ++tap) {
+    const bool last_in_group = tap == 3 * G + 2;
+    if (tap + 1 < 9) {
+#pragma unroll
+      for (int t = 0; t < K::NT; ++t)
+        if (((last_in_group ? LVN : LV) >> t) & 1u) off_nxt[t] = nb.off(t, tap + 1) + hoff;
+    }
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      const int s = tap * KK + kk;
+      if (kk + 1 < KK) {
+#pragma unroll
+        for (int t = 0; t < K::NT; ++t)
+          if ((LV >> t) & 1u) bn[t] = lds_b128(src + off_cur[t] + (kk + 1) * 32);
+      } else if (!last_in_group) {
+#pragma unroll
+        for (int t = 0; t < K::NT; ++t)
+          if ((LV >> t) & 1u) bn[t] = lds_b128(src + off_nxt[t]);
+      } else if (G < 2) {
+#pragma unroll
+        for (int t = 0; t < K::NT; ++t)
+          if ((LVN >> t) & 1u) bn[t] = lds_b128(src + off_nxt[t]);
+      }
+      const int slot = kk % DEPTH;
+      bf16x8 acur[K::MT];
+#pragma unroll
+      for (int m = 0; m < K::MT; ++m) acur[m] = a[slot][m];
+      const int sn = s + DEPTH;
+      if (sn < STEPS) {
+#pragma unroll
+        for (int m = 0; m < K::MT; ++m) a[slot][m] = wb.load(wl_off + m * MSTRIDE + (uint32_t)sn * 1024u);
+      } else if (sn - STEPS < wn_steps) {
+#pragma unroll
+        for (int m = 0; m < K::MT; ++m) a[slot][m] = wb.load(wn_off + m * MSTRIDE + (uint32_t)(sn - STEPS) * 1024u);
+      }
+      if (G == 0 && s == 0) {
+#pragma unroll
+        for (int t = 0; t < K::NT; ++t)
+#pragma unroll
+          for (int m = 0; m < K::MT; ++m)
+            if ((LV >> t) & 1u) acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[m], bc[t], f32x16{}, 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int t = 0; t < K::NT; ++t)
+#pragma unroll
+          for (int m = 0; m < K::MT; ++m)
+            if ((LV >> t) & 1u) acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[m], bc[t], acc[m][t], 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < NTA; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+      }
+#pragma unroll
+      for (int i = 0; i < K::MT; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, K::MT * NTA - NTA - K::MT, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < K::NT; ++t) bc[t] = bn[t];
+    }
+#pragma unroll
+    for (int t = 0; t < K::NT; ++t) off_cur[t] = off_nxt[t];
+  }
+}
+
+template <class K, int KK, int DEPTH, bool RESID, int MG_>
+__device__ __forceinline__ void conv_layer_x(const char *src, char *dst, const Nbr<K> &nb, bf16x8 (&a)[DEPTH][K::MT],
+                                             const float *bias, int wave, int lane, const WBuf &wb, uint32_t wl_off,
+                                             uint32_t wn_off, int wn_steps) {
+  using X = XLive<K, MG_>;
+  static_assert(KK % DEPTH == 0, "ring slot must be a compile-time function of kk");
+  const int hoff = 16 * (lane >> 5);
+  f32x16 acc[K::MT][K::NT];
+#pragma unroll
+  for (int t = 0; t < K::NT; ++t)
+#pragma unroll
+    for (int m = 0; m < K::MT; ++m)
+      if ((X::ZPRE >> t) & 1u) acc[m][t] = f32x16{};
+  int off_cur[K::NT], off_nxt[K::NT];
+  bf16x8 bc[K::NT], bn[K::NT];
+#pragma unroll
+  for (int t = 0; t < K::NT; ++t)
+    if ((X::LIVE[0] >> t) & 1u) {
+      off_cur[t] = nb.off(t, 0) + hoff;
+      bc[t] = lds_b128(src + off_cur[t]);
+    }
+  conv_group_x<K, KK, DEPTH, MG_, 0>(src, nb, acc, bc, bn, off_cur, off_nxt, a, hoff, wb, wl_off, wn_off, wn_steps);
+  conv_group_x<K, KK, DEPTH, MG_, 1>(src, nb, acc, bc, bn, off_cur, off_nxt, a, hoff, wb, wl_off, wn_off, wn_steps);
+  conv_group_x<K, KK, DEPTH, MG_, 2>(src, nb, acc, bc, bn, off_cur, off_nxt, a, hoff, wb, wl_off, wn_off, wn_steps);
+  acc_store_bias_relu<K, RESID>(acc, dst, bias, wave, lane);
+}
+
 // Stem: 3 input planes padded to one 16-channel k-step per tap (9 steps, weights loaded in place).
 template <class K>
 __device__ __forceinline__ void stem_layer(const char *src, char *dst, const Nbr<K> &nb, const bf16x8 *w,
@@ -457,9 +608,9 @@ __device__ __forceinline__ void head_layer(const char *src, const bf16x8 *w, con
     for (int t = 0; t < TPW; ++t) {
       const int row = (t0 + t) * 32 + r;
       if (row >= K::VROWS) continue;
-      const int board = board0 + row / K::CELLS;
+      const int board = board0 + K::row_board(row);
       if (board >= batch) continue;
-      const int cell = row % K::CELLS;
+      const int cell = K::row_cell(row);
       bf16x4 o;
       o[0] = (__bf16)fmaxf(acc[t][4 * g + 0] + bv.x, 0.f);
       o[1] = (__bf16)fmaxf(acc[t][4 * g + 1] + bv.y, 0.f);
@@ -492,10 +643,10 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
     ((uint32_t *)(Y + K::ZROW * K::RS))[i] = 0u;
   }
   for (int row = tid; row < K::ROWS; row += K::THREADS) {
-    const int board = board0 + row / K::CELLS;
+    const int board = board0 + K::row_board(row);
     __bf16 *dst = (__bf16 *)(Y + row * K::RS);
     const bool ok = row < K::VROWS && board < batch;
-    const size_t src = ((size_t)board * K::CELLS + row % K::CELLS) * 3;
+    const size_t src = ((size_t)board * K::CELLS + K::row_cell(row)) * 3;
 #pragma unroll
     for (int c = 0; c < 16; ++c) dst[c] = (ok && c < 3) ? planes[src + c] : (__bf16)0.f;
   }
@@ -536,10 +687,21 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
       wn[m] = wblk + (size_t)(L + 1) * LAYER + ct;
     }
     const int wn_steps = L + 1 < n_convs ? LSTEPS : 0;
-    if ((L & 1) == 0)
+    if constexpr (K::XMAJ) {
+      static_assert(K::MG == 2 && K::ABL == 0, "column-group conv: two row halves, no ablations");
+      const bool even = (L & 1) == 0;
+      if (wave / K::CG == 0) {
+        if (even) conv_layer_x<K, KK, DEPTH, false, 0>(X, Y, nb, ring, b, wave, lane, wb, wl_off, wn_off, wn_steps);
+        else conv_layer_x<K, KK, DEPTH, true, 0>(Y, X, nb, ring, b, wave, lane, wb, wl_off, wn_off, wn_steps);
+      } else {
+        if (even) conv_layer_x<K, KK, DEPTH, false, 1>(X, Y, nb, ring, b, wave, lane, wb, wl_off, wn_off, wn_steps);
+        else conv_layer_x<K, KK, DEPTH, true, 1>(Y, X, nb, ring, b, wave, lane, wb, wl_off, wn_off, wn_steps);
+      }
+    } else if ((L & 1) == 0) {
       conv_layer<K, KK, DEPTH, false>(X, Y, nb, wl, wn, wn_steps, ring, b, wave, lane, wb, wl_off, wn_off);
-    else
+    } else {
       conv_layer<K, KK, DEPTH, true>(Y, X, nb, wl, wn, wn_steps, ring, b, wave, lane, wb, wl_off, wn_off);
+    }
     b += K::C;
     if constexpr (!(K::ABL & 4)) __syncthreads();
   }
@@ -808,11 +970,14 @@ static int launch_split(const char *planes, int batch, int n_blocks, const void 
   }
 }
 
+// pack: the launch runs beside launches on other streams (SPMCTS_TOWER_PACK): tiles are assigned
+// as if the chip had one CU (all boards in full tiles, the last < BOARDS in one smaller tile); the
+// other streams' workgroups fill the CUs a partial round would leave idle.
 template <class KF, class KM, class KH>
 static int launch_dyn(const void *planes, const int32_t *count, int max_batch, int n_blocks, const void *w,
-                      const float *b, void *out, hipStream_t s) {
-  const int cus = num_cus();
-  const int grid = (max_batch + KF::BOARDS - 1) / KF::BOARDS + cus;
+                      const float *b, void *out, bool pack, hipStream_t s) {
+  const int cus = pack ? 1 : num_cus();
+  const int grid = (max_batch + KF::BOARDS - 1) / KF::BOARDS + (pack ? 1 : cus);
   constexpr int LDS = KF::LDS > KM::LDS ? (KF::LDS > KH::LDS ? KF::LDS : KH::LDS) : (KM::LDS > KH::LDS ? KM::LDS : KH::LDS);
   static bool attr_set = false;
   if (!attr_set) {
@@ -831,23 +996,24 @@ static int launch_dyn(const void *planes, const int32_t *count, int max_batch, i
 extern "C" int spmcts_tower_forward_dev(int32_t width, int32_t height, int32_t channels, int32_t n_blocks,
                                         const void *planes_dev, const int32_t *count_dev, int32_t max_batch,
                                         const void *weights_dev, const float *bias_dev, void *features_dev,
-                                        spmcts_stream stream) {
+                                        int32_t flags, spmcts_stream stream) {
   using namespace tower;
   hipStream_t s = (hipStream_t)stream;
-  if (n_blocks < 0 || max_batch < 0 || !count_dev) return -3;
+  if (n_blocks < 0 || max_batch < 0 || !count_dev || (flags & ~SPMCTS_TOWER_PACK)) return -3;
   if (max_batch == 0) return 0;
+  const bool pack = (flags & SPMCTS_TOWER_PACK) != 0;
   if (width == 7 && height == 6 && channels == 128)
-    return launch_dyn<Cfg<128, 256, 7, 6, 2>, Cfg<128, 192, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(planes_dev, count_dev, max_batch, n_blocks,
-                                                                      weights_dev, bias_dev, features_dev, s);
+    return launch_dyn<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true>, Cfg<128, 192, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(planes_dev, count_dev, max_batch, n_blocks,
+                                                                      weights_dev, bias_dev, features_dev, pack, s);
   if (width == 7 && height == 6 && channels == 256)
     return launch_dyn<Cfg<256, 128, 7, 6, 4>, Cfg<256, 128, 7, 6, 4>, Cfg<256, 128, 7, 6, 4>>(planes_dev, count_dev, max_batch, n_blocks,
-                                                                      weights_dev, bias_dev, features_dev, s);
+                                                                      weights_dev, bias_dev, features_dev, pack, s);
   if (width == 3 && height == 3 && channels == 128)
     return launch_dyn<Cfg<128, 256, 3, 3, 2>, Cfg<128, 192, 3, 3, 2>, Cfg<128, 128, 3, 3, 2>>(planes_dev, count_dev, max_batch, n_blocks,
-                                                                      weights_dev, bias_dev, features_dev, s);
+                                                                      weights_dev, bias_dev, features_dev, pack, s);
   if (width == 3 && height == 3 && channels == 256)
     return launch_dyn<Cfg<256, 128, 3, 3, 4>, Cfg<256, 128, 3, 3, 4>, Cfg<256, 128, 3, 3, 4>>(planes_dev, count_dev, max_batch, n_blocks,
-                                                                      weights_dev, bias_dev, features_dev, s);
+                                                                      weights_dev, bias_dev, features_dev, pack, s);
   return -2;
 }
 
@@ -885,7 +1051,8 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
       case 25: return launch<Cfg<128, 256, 7, 6, 2, 4, 0, 8>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       case 26: return launch<Cfg<128, 256, 7, 6, 2, 4, 0, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       case 10: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);  // two tile sizes only
-      default: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 192, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      case 11: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 192, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);  // board-major full tiles
+      default: return launch_split<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true>, Cfg<128, 192, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
     }
   }
   if (width == 7 && height == 6 && channels == 256)

@@ -375,11 +375,13 @@ class LanedEngine:
     enable_timers / refresh_network).  Lane i uses the Philox subsequences of trees
     [offset_i, offset_i + 2 n_i) of a single arena of n_games slots (same seed), and its exported
     game ids are offset by i * 2**40 (even, so swap_sides = id odd is preserved and ids stay unique).
-    Each lane is a complete arena: results are those of `lanes` independent engines."""
+    Each lane is a complete arena: results are those of `lanes` independent engines.  With `pack`
+    the fused tower packs every lane's batch into full tiles (SPMCTS_TOWER_PACK) rather than whole
+    chip rounds, since the lanes' concurrent launches fill each other's partial rounds."""
 
     GAME_ID_STRIDE = 1 << 40
 
-    def __init__(self, game, network, n_games=4096, lanes=2, seed=0, subsequence0=None, device=None, **kw):
+    def __init__(self, game, network, n_games=4096, lanes=2, seed=0, subsequence0=None, device=None, pack=True, **kw):
         if lanes < 1 or n_games < lanes:
             raise ValueError(f"need 1 <= lanes <= n_games (lanes={lanes}, n_games={n_games})")
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -396,6 +398,11 @@ class LanedEngine:
                                                  device=self.device, **kw))
             off += n
         torch.cuda.synchronize(self.device)
+        if lanes > 1 and pack:
+            for e in self.lanes:  # tower launches share the chip: full tiles, no round alignment
+                for ev in (e.evaluator, e.evaluator1):
+                    if ev is not None and hasattr(ev, "concurrent"):
+                        ev.concurrent = True
         self.n_games = n_games
         self.iterations = self.lanes[0].iterations
         self.evaluator = self.lanes[0].evaluator

@@ -277,6 +277,9 @@ class HipTowerEvaluator(Evaluator):
         t.train(was)
 
     supports_device_count = True
+    # set by engine.LanedEngine: the tower launches share the chip with other lanes' launches, so
+    # tiles are packed full (SPMCTS_TOWER_PACK) instead of aligned to whole chip rounds
+    concurrent = False
 
     def reserve(self, rows, device):
         """(Re)allocate the device-count path's output buffers for at least `rows` rows."""
@@ -302,9 +305,10 @@ class HipTowerEvaluator(Evaluator):
         timer = getattr(self, "tower_timer", None)
         if timer is not None:
             timer.start()
+        flags = self._lib.TOWER_PACK if self.concurrent else 0
         rc = L.spmcts_tower_forward_dev(self.W, self.H, self.C, self.n_blocks, c(leaves.data_ptr()),
                                         c(count_dev.data_ptr()), max_rows, c(self.wblob.data_ptr()),
-                                        c(self.bblob.data_ptr()), c(feats.data_ptr()), stream)
+                                        c(self.bblob.data_ptr()), c(feats.data_ptr()), flags, stream)
         if timer is not None:
             timer.stop()
         if rc != 0:

@@ -84,9 +84,11 @@ def test_forward_dev_matches_host_count(n):
     hip = HipTowerEvaluator(net)
     p, v = hip(x[:n].contiguous(memory_format=torch.channels_last))
     cnt = torch.tensor([n], dtype=torch.int32, device=x.device)
-    pd, vd = hip.forward_dev(x, cnt, max_rows)
-    torch.cuda.synchronize()
-    assert torch.equal(pd[:n], p) and torch.equal(vd[:n].view(-1), v.view(-1))
+    for pack in (False, True):  # round-aligned tiles / SPMCTS_TOWER_PACK (full tiles + one small tail)
+        hip.concurrent = pack
+        pd, vd = hip.forward_dev(x, cnt, max_rows)
+        torch.cuda.synchronize()
+        assert torch.equal(pd[:n], p) and torch.equal(vd[:n].view(-1), v.view(-1)), pack
 
 
 def test_engine_async_matches_sync_path():
