@@ -210,6 +210,40 @@ __device__ __forceinline__ void acc_store_bias_relu(const f32x16 (&acc)[K::MT][K
     }
 }
 
+// acc_store_bias_relu with the bias already in registers (bv[m][g] = bias[ch(m, g) .. + 4], loaded
+// at the start of the layer so its global-load latency hides under the k-loop instead of stalling
+// the epilogue).
+template <class K, bool RESID>
+__device__ __forceinline__ void acc_store_bias_relu_pre(const f32x16 (&acc)[K::MT][K::NT], char *dst,
+                                                        const float4 (&bv)[K::MT][4], int wave, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int m = 0; m < K::MT; ++m)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int ch = ((wave % K::CG) * K::MT + m) * 32 + 8 * g + 4 * h;
+#pragma unroll
+      for (int t = 0; t < K::NT; ++t) {
+        char *p = dst + (((wave / K::CG) * K::NT + t) * 32 + r) * K::RS + ch * 2;
+        float v0 = acc[m][t][4 * g + 0] + bv[m][g].x, v1 = acc[m][t][4 * g + 1] + bv[m][g].y;
+        float v2 = acc[m][t][4 * g + 2] + bv[m][g].z, v3 = acc[m][t][4 * g + 3] + bv[m][g].w;
+        if (RESID) {
+          const bf16x4 x = *(const bf16x4 *)p;
+          v0 += (float)x[0];
+          v1 += (float)x[1];
+          v2 += (float)x[2];
+          v3 += (float)x[3];
+        }
+        bf16x4 o;
+        o[0] = (__bf16)fmaxf(v0, 0.f);
+        o[1] = (__bf16)fmaxf(v1, 0.f);
+        o[2] = (__bf16)fmaxf(v2, 0.f);
+        o[3] = (__bf16)fmaxf(v3, 0.f);
+        *(bf16x4 *)p = o;
+      }
+    }
+}
+
 // Packed-math form of acc_store_bias_relu: v_pk_add_f32 for bias (and residual), one
 // v_cvt_pk_bf16_f32 per pair, ReLU on the packed bf16 pair as a signed 16-bit max with 0
 // (v_pk_max_i16: a bf16 with the sign bit set is a negative int16).
@@ -294,6 +328,14 @@ __device__ __forceinline__ void conv_layer(const char *src, char *dst, const Nbr
   }
 
   const int hoff = 16 * h;  // byte offset of this lane's 8 channels inside a 16-channel k-step
+  // default epilogue: its bias fetched now, so the global-load latency hides under the k-loop
+  float4 bv[K::MT][4];
+  if constexpr (ZINIT && !(K::ABL & (2 | 2048))) {
+#pragma unroll
+    for (int m = 0; m < K::MT; ++m)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) bv[m][g] = *(const float4 *)(bias + ((wave % K::CG) * K::MT + m) * 32 + 8 * g + 4 * h);
+  }
   int off_cur[K::NT], off_nxt[K::NT];
 #pragma unroll
   for (int t = 0; t < K::NT; ++t) off_cur[t] = nb.off(t, 0) + hoff;
@@ -411,7 +453,7 @@ __device__ __forceinline__ void conv_layer(const char *src, char *dst, const Nbr
   } else if constexpr (ZINIT && (K::ABL & 2048)) {
     acc_store_bias_relu_pk<K, RESID>(acc, dst, bias, wave, lane);
   } else if constexpr (ZINIT) {
-    acc_store_bias_relu<K, RESID>(acc, dst, bias, wave, lane);
+    acc_store_bias_relu_pre<K, RESID>(acc, dst, bv, wave, lane);
   } else {
     acc_store_relu<K>(acc, dst, wave, lane);
   }
@@ -526,6 +568,11 @@ __device__ __forceinline__ void conv_layer_x(const char *src, char *dst, const N
   using X = XLive<K, MG_>;
   static_assert(KK % DEPTH == 0, "ring slot must be a compile-time function of kk");
   const int hoff = 16 * (lane >> 5);
+  float4 bv[K::MT][4];  // the epilogue's bias, fetched now (its latency hides under the k-loop)
+#pragma unroll
+  for (int m = 0; m < K::MT; ++m)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) bv[m][g] = *(const float4 *)(bias + ((wave % K::CG) * K::MT + m) * 32 + 8 * g + 4 * (lane >> 5));
   f32x16 acc[K::MT][K::NT];
 #pragma unroll
   for (int t = 0; t < K::NT; ++t)
@@ -543,7 +590,7 @@ __device__ __forceinline__ void conv_layer_x(const char *src, char *dst, const N
   conv_group_x<K, KK, DEPTH, MG_, 0>(src, nb, acc, bc, bn, off_cur, off_nxt, a, hoff, wb, wl_off, wn_off, wn_steps);
   conv_group_x<K, KK, DEPTH, MG_, 1>(src, nb, acc, bc, bn, off_cur, off_nxt, a, hoff, wb, wl_off, wn_off, wn_steps);
   conv_group_x<K, KK, DEPTH, MG_, 2>(src, nb, acc, bc, bn, off_cur, off_nxt, a, hoff, wb, wl_off, wn_off, wn_steps);
-  acc_store_bias_relu<K, RESID>(acc, dst, bias, wave, lane);
+  acc_store_bias_relu_pre<K, RESID>(acc, dst, bv, wave, lane);
 }
 
 // Stem: 3 input planes padded to one 16-channel k-step per tap (9 steps, weights loaded in place).
