@@ -138,11 +138,14 @@ struct Nbr {
       mask[t] = m;
     }
   }
-  // byte offset of the source row of tile t for `tap` (the zero row when off the board)
+  // byte offset of the source row of tile t for `tap` (the zero row when off the board); a
+  // branch-free select (hipcc otherwise emits an exec-mask branch per tile and tap)
   __device__ __forceinline__ int off(int t, int tap) const {
     const int dr = (tap / 3 - 1) * K::DX + (tap % 3 - 1);
-    const int d = dr * K::RS;
-    return ((mask[t] >> tap) & 1u) ? base[t] + d : (K::ZROW + ((rowi[t] + dr) & (K::NZ - 1))) * K::RS;
+    const int on = base[t] + dr * K::RS;
+    const int zero = (K::ZROW + ((rowi[t] + dr) & (K::NZ - 1))) * K::RS;
+    const int live = (int)((mask[t] >> tap) & 1u);
+    return zero + live * (on - zero);
   }
 };
 
