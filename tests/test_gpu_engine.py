@@ -309,3 +309,48 @@ def test_laned_engine_plays_like_its_lanes():
             assert gid not in firsts
             firsts[gid] = True
     assert len(firsts) == c["games_finished"] and (ids >= 0).all()
+
+
+def _gravity_ok(board):
+    """Connect4 board [W, H] (row 0 = bottom): every column's pieces are contiguous from the bottom."""
+    filled = board != 0
+    return bool((filled[:, 1:] <= filled[:, :-1]).all())
+
+
+def test_full_size_selfplay_properties():
+    """The bench workload at its full size (BASELINE configs[1]: Connect4, 200 sims/move, 4,096
+    games, ResNet-128x20 on the fused tower, two lanes with packed tiles), checked through
+    size-independent properties: exact simulation / move / leaf accounting, every exported Move a
+    legal gravity-consistent position with a normalised, legal-only visit distribution, consistent
+    per-game results, no device error flags."""
+    from self_play_reinforcement_learning_amd.engine import LanedEngine
+    from self_play_reinforcement_learning_amd.modules import ResidualTower
+
+    torch.manual_seed(0)
+    net = ResidualTower(7, 6, 7, num_blocks=20, filter_factor=32).cuda().eval()
+    G, sims, plies = 4096, 200, 12
+    eng = LanedEngine("connect4", net, n_games=G, lanes=2, iterations=sims, seed=11)
+    got = []
+    eng.run(plies=plies, on_moves=lambda m: got.append({k: v.cpu().numpy() for k, v in m.items()}))
+    eng.check()
+    c = eng.counters()
+    assert c["error_flags"] == 0
+    assert c["sims"] == G * sims * plies  # every slot searches every ply (finished slots refill)
+    assert c["moves"] == G * plies
+    # each simulation ends in exactly one network leaf or one terminal leaf; the end-of-ply
+    # _set_node expansions add network leaves of their own (none for a terminal child)
+    sim_nn = c["sims"] - c["terminal_leaves"]
+    assert sim_nn <= c["nn_leaves"] <= sim_nn + c["set_node_expansions"]
+    moves = {k: np.concatenate([g[k] for g in got]) for k in got[0]}
+    assert len(moves["z"]) == c["positions_exported"] > 0
+    assert c["games_finished"] == len(np.unique(moves["game"]))
+    assert set(np.unique(moves["z"]).tolist()) <= {-1.0, 0.0, 1.0}
+    np.testing.assert_allclose(moves["tree_probs"].sum(1), 1.0, atol=1e-5)
+    boards = moves["state"].reshape(-1, 7, 6).astype(int)
+    for b, p in zip(boards, moves["tree_probs"]):
+        assert _gravity_ok(b)
+        assert (p[b[:, 5] != 0] == 0).all()  # full columns get no visits
+        assert (b == 1).sum() in ((b == -1).sum(), (b == -1).sum() - 1)
+    for gid in np.unique(moves["game"]):
+        zs = moves["z"][moves["game"] == gid]
+        assert (zs == 0).all() or sorted(np.unique(zs).tolist()) == [-1.0, 1.0]
