@@ -213,6 +213,13 @@ __device__ __forceinline__ void acc_store_bias_relu(const f32x16 (&acc)[K::MT][K
     }
 }
 
+// ReLU of a pair as bf16: convert, then a signed 16-bit max with 0 (a negative bf16 is a negative int16).
+__device__ __forceinline__ uint32_t relu_pk_bf16(f32x2 v) {
+  const bf16x2 b = __builtin_convertvector(v, bf16x2);
+  const i16x2 m = __builtin_elementwise_max(__builtin_bit_cast(i16x2, b), i16x2{0, 0});
+  return __builtin_bit_cast(uint32_t, m);
+}
+
 // acc_store_bias_relu with the bias already in registers (bv[m][g] = bias[ch(m, g) .. + 4], loaded
 // at the start of the layer so its global-load latency hides under the k-loop instead of stalling
 // the epilogue).
@@ -251,12 +258,9 @@ __device__ __forceinline__ void acc_store_bias_relu_pre(const f32x16 (&acc)[K::M
           v2 += (float)x[2];
           v3 += (float)x[3];
         }
-        bf16x4 o;
-        o[0] = (__bf16)fmaxf(v0, 0.f);
-        o[1] = (__bf16)fmaxf(v1, 0.f);
-        o[2] = (__bf16)fmaxf(v2, 0.f);
-        o[3] = (__bf16)fmaxf(v3, 0.f);
-        *(bf16x4 *)p = o;
+        // ReLU on the converted bf16 pairs (v_cvt_pk_bf16_f32 + v_pk_max_i16: identical bits to
+        // converting max(v, 0), one instruction per pair instead of one per value)
+        *(uint2 *)p = make_uint2(relu_pk_bf16(f32x2{v0, v1}), relu_pk_bf16(f32x2{v2, v3}));
       }
     }
 }
@@ -264,11 +268,6 @@ __device__ __forceinline__ void acc_store_bias_relu_pre(const f32x16 (&acc)[K::M
 // Packed-math form of acc_store_bias_relu: v_pk_add_f32 for bias (and residual), one
 // v_cvt_pk_bf16_f32 per pair, ReLU on the packed bf16 pair as a signed 16-bit max with 0
 // (v_pk_max_i16: a bf16 with the sign bit set is a negative int16).
-__device__ __forceinline__ uint32_t relu_pk_bf16(f32x2 v) {
-  const bf16x2 b = __builtin_convertvector(v, bf16x2);
-  const i16x2 m = __builtin_elementwise_max(__builtin_bit_cast(i16x2, b), i16x2{0, 0});
-  return __builtin_bit_cast(uint32_t, m);
-}
 
 template <class K, bool RESID>
 __device__ __forceinline__ void acc_store_bias_relu_pk(const f32x16 (&acc)[K::MT][K::NT], char *dst, const float *bias,
