@@ -227,22 +227,21 @@ template <class K, bool RESID>
 __device__ __forceinline__ void acc_store_bias_relu_pre(const f32x16 (&acc)[K::MT][K::NT], char *dst,
                                                         const float4 (&bv)[K::MT][4], int wave, int lane) {
   const int r = lane & 31, h = lane >> 5;
-  // residual (block input) of every output group read before any output is written: issued back
-  // to back, the LDS latency is paid once instead of once per read -> add -> write chain
-  bf16x4 res[RESID ? K::MT : 1][4][K::NT];
-  if constexpr (RESID) {
+  // per channel tile m: the residuals (block input) of its 4 x NT output groups are read in one batch
+  // before any of them is written, so the LDS latency is paid once per batch instead of once per
+  // read -> add -> write chain (one batch per m keeps the staging at 2 x NT x 4 registers)
 #pragma unroll
-    for (int m = 0; m < K::MT; ++m)
+  for (int m = 0; m < K::MT; ++m) {
+    bf16x4 res[RESID ? 4 : 1][K::NT];
+    if constexpr (RESID) {
 #pragma unroll
       for (int g = 0; g < 4; ++g)
 #pragma unroll
         for (int t = 0; t < K::NT; ++t)
-          res[m][g][t] = *(const bf16x4 *)(dst + (((wave / K::CG) * K::NT + t) * 32 + r) * K::RS +
-                                           (((wave % K::CG) * K::MT + m) * 32 + 8 * g + 4 * h) * 2);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-#pragma unroll
-  for (int m = 0; m < K::MT; ++m)
+          res[g][t] = *(const bf16x4 *)(dst + (((wave / K::CG) * K::NT + t) * 32 + r) * K::RS +
+                                        (((wave % K::CG) * K::MT + m) * 32 + 8 * g + 4 * h) * 2);
+      __builtin_amdgcn_sched_barrier(0);
+    }
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int ch = ((wave % K::CG) * K::MT + m) * 32 + 8 * g + 4 * h;
@@ -252,7 +251,7 @@ __device__ __forceinline__ void acc_store_bias_relu_pre(const f32x16 (&acc)[K::M
         float v0 = acc[m][t][4 * g + 0] + bv[m][g].x, v1 = acc[m][t][4 * g + 1] + bv[m][g].y;
         float v2 = acc[m][t][4 * g + 2] + bv[m][g].z, v3 = acc[m][t][4 * g + 3] + bv[m][g].w;
         if constexpr (RESID) {
-          const bf16x4 x = res[m][g][t];
+          const bf16x4 x = res[g][t];
           v0 += (float)x[0];
           v1 += (float)x[1];
           v2 += (float)x[2];
@@ -263,6 +262,7 @@ __device__ __forceinline__ void acc_store_bias_relu_pre(const f32x16 (&acc)[K::M
         *(uint2 *)p = make_uint2(relu_pk_bf16(f32x2{v0, v1}), relu_pk_bf16(f32x2{v2, v3}));
       }
     }
+  }
 }
 
 // Packed-math form of acc_store_bias_relu: v_pk_add_f32 for bias (and residual), one
