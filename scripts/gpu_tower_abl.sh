@@ -2,7 +2,7 @@
 set -u
 mkdir -p gpurun_out/abl
 export TMPDIR=/tmp
-for code in ${CODES:-2 5 100 101 102 103 104 107 108 116 124 131}; do
+for code in ${CODES:-2 11 100 101 102 104 108 116 124}; do
   SPMCTS_TOWER_CG=$code timeout -k 10 120 python scripts/bench_tower.py --trunk-only --iters ${ITERS:-10} --batch ${BATCH:-1536} >> gpurun_out/abl/abl.jsonl 2> gpurun_out/abl/err_$code.txt
   rc=$?
   if [ $rc -ne 0 ]; then echo "code $code rc=$rc"; tail -3 gpurun_out/abl/err_$code.txt; exit $rc; fi

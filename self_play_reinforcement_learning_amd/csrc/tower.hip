@@ -1096,33 +1096,19 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
   const char *pl = (const char *)planes_dev;
   char *ft = (char *)features_dev;
   if (width == 7 && height == 6 && channels == 128) {
-    switch (cg) {
-      case 1: return launch<Cfg<128, 256, 7, 6, 1>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-      case 4: return launch<Cfg<128, 256, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-      case 3: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 128, 7, 6, 4>, Cfg<128, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-      case 5: return launch<Cfg<128, 256, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-      case 8: return launch_split<Cfg<128, 256, 7, 6, 2, 8>, Cfg<128, 128, 7, 6, 2, 8>, Cfg<128, 128, 7, 6, 2, 8>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-      case 9: return launch_split<Cfg<128, 256, 7, 6, 4, 8>, Cfg<128, 128, 7, 6, 4, 8>, Cfg<128, 128, 7, 6, 4, 8>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+    switch (cg) {  // timing alternatives (SPMCTS_TOWER_CG); DESIGN.md §4 has the measurements
 #define ABLATE(X) \
       case 100 + X: return launch<Cfg<128, 256, 7, 6, 2, 4, X>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       ABLATE(0) ABLATE(1) ABLATE(2) ABLATE(4) ABLATE(8) ABLATE(16) ABLATE(24) ABLATE(31) ABLATE(64) ABLATE(128)
       ABLATE(256) ABLATE(2048) ABLATE(32768)
 #undef ABLATE
-      case 20: return launch<Cfg<128, 128, 7, 6, 2, 4, 0, 4, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-      case 21: return launch<Cfg<128, 128, 7, 6, 4, 4, 0, 4, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-      case 22: return launch<Cfg<128, 128, 7, 6, 2, 4, 0, 2, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-      case 23: return launch<Cfg<128, 256, 7, 6, 4, 4, 0, 8>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-      case 24: return launch<Cfg<128, 256, 7, 6, 4, 4, 0, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-      case 25: return launch<Cfg<128, 256, 7, 6, 2, 4, 0, 8>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-      case 26: return launch<Cfg<128, 256, 7, 6, 2, 4, 0, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       case 10: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);  // two tile sizes only
       case 11: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 192, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);  // board-major full tiles
       default: return launch_split<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true>, Cfg<128, 192, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
     }
   }
   if (width == 7 && height == 6 && channels == 256)
-    return cg == 2 ? launch<Cfg<256, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s)
-                   : launch<Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);  // CG=4 default
+    return launch<Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);  // as the device-count path
   if (width == 3 && height == 3 && channels == 128)
     return launch<Cfg<128, 256, 3, 3>>(planes_dev, batch, n_blocks, weights_dev, bias_dev, features_dev, s);
   if (width == 3 && height == 3 && channels == 256)
