@@ -82,7 +82,7 @@ class SelfPlayScheduler:
     def __init__(self, policy_container, env, evaluation_policy_container=None, network=None, swap_sides=True,
                  save_dir="saves", epoch_length=500, initial_games=64, lr=0.001, stagger=False, evaluation_games=100,
                  evaluation_network=None, stagger_mem_step=5000, deduplicate=False, update_delay=0.01,
-                 self_play=None, n_games=None, device=None, seed=0, updates_per_ply=4, lanes=1):
+                 self_play=None, n_games=None, device=None, seed=0, updates_per_ply=4, lanes=None):
         self.policy_container = policy_container
         self.evaluation_policy_container = evaluation_policy_container
         self.env_gen = env
@@ -102,7 +102,9 @@ class SelfPlayScheduler:
         self.network = self._get_network(network, policy_container)
         self.seed = seed
         self.updates_per_ply = updates_per_ply
-        self.lanes = max(1, int(lanes))  # >1: LanedEngine (arenas on separate HIP streams, same results per lane)
+        # >1: LanedEngine (arenas on separate HIP streams, each a complete arena); None = 2 lanes for
+        # arenas of >= 1,024 games, where the overlap pays (bench.py), else one arena
+        self.lanes = None if lanes is None else max(1, int(lanes))
         rank, world, local = D.env_rank()
         self.rank, self.world = rank, world
         self.device = torch.device(device) if device is not None else D.local_device()
@@ -142,8 +144,9 @@ class SelfPlayScheduler:
             self._load_latest(prev_run=True)
         ekw = dict(iterations=kw.get("iterations", 100), alpha=kw.get("alpha", 1),
                    strong_play=kw.get("strong_play", False), seed=self.seed + 7919 * self.rank, device=self.device)
-        if self.lanes > 1 and n_games >= 2 * self.lanes:
-            self.engine = LanedEngine(self.game, self.network, n_games=n_games, lanes=self.lanes, **ekw)
+        lanes = self.lanes if self.lanes is not None else (2 if n_games >= 1024 else 1)
+        if lanes > 1 and n_games >= 2 * lanes:
+            self.engine = LanedEngine(self.game, self.network, n_games=n_games, lanes=lanes, **ekw)
         else:
             self.engine = SelfPlayEngine(self.game, self.network, n_games=n_games, **ekw)
         return self.engine, None, self.epoch_value
