@@ -1,0 +1,36 @@
+"""Effective clock and MFMA-pipe utilisation of k_tower launches from one rocprofv3 PMC pass
+(scripts/gpu_tower_util.sh).  GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md
+'DVFS give-back'); SQ_VALU_MFMA_BUSY_CYCLES counts MFMA-busy cycles summed over all SIMDs."""
+import collections
+import csv
+import json
+import sys
+
+SIMDS = 256 * 4
+
+
+def main(path, out):
+    disp = collections.defaultdict(dict)
+    for r in csv.DictReader(open(path)):
+        d = disp[r["Dispatch_Id"]]
+        d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        d["ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    rows = []
+    for d in disp.values():
+        cyc = d["GRBM_GUI_ACTIVE"] / 8
+        rows.append(dict(ns=d["ns"], clock_ghz=cyc / d["ns"],
+                         mfma_busy_frac=d["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * SIMDS),
+                         mfma_insts=d["SQ_INSTS_MFMA"]))
+    rows = rows[2:] or rows  # skip warm-up dispatches
+    n = len(rows)
+    res = {k: sum(r[k] for r in rows) / n for k in rows[0]}
+    res["dispatches"] = n
+    res["note"] = ("trunk-only, 1,536 boards = one full round of 6-board column-major tiles per dispatch; "
+                   "clock = GRBM_GUI_ACTIVE / 8 / duration; mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / "
+                   "(cycles x 1024 SIMDs)")
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:3])

@@ -654,9 +654,13 @@ __device__ __forceinline__ void head_layer(const char *src, const bf16x8 *w, con
   for (int t = 0; t < TPW; ++t)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
-#pragma unroll 4
+  // all KK weight fragments requested up front: one global-load latency instead of one per group
+  bf16x8 wf[KK];
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) wf[kk] = w[((size_t)ct * KK + kk) * 64 + lane];
+#pragma unroll
   for (int kk = 0; kk < KK; ++kk) {
-    const bf16x8 a = w[((size_t)ct * KK + kk) * 64 + lane];
+    const bf16x8 a = wf[kk];
     const int koff = (kk * 16 + 8 * h) * 2;
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {

@@ -249,8 +249,9 @@ class SelfPlayEngine:
         self.arena.games_end_ply_async()
         self._eval_expand_dev()
 
-    def ply(self, on_moves=None, refill=True):
-        """Advance every active game by one move. Returns (#games finished, #records exported)."""
+    def ply(self, on_moves=None, refill=True, game_offset=0):
+        """Advance every active game by one move. Returns (#games finished, #records exported).
+        `game_offset` is added to the exported game ids (LanedEngine lanes)."""
         self._ply_begin()
         a = self.arena
         if self._device_count_ok():
@@ -261,7 +262,7 @@ class SelfPlayEngine:
             for _ in range(self.iterations):
                 self._eval_expand(a.select(self.select_timer))
             self._eval_expand(a.games_end_ply())
-        return self._ply_finish(on_moves, refill)
+        return self._ply_finish(on_moves, refill, game_offset)
 
     def _ply_finish(self, on_moves=None, refill=True, game_offset=0):
         a = self.arena
@@ -389,13 +390,17 @@ class LanedEngine:
         if subsequence0 is None:
             subsequence0 = rank * 2 * n_games
         sizes = [n_games // lanes + (1 if i < n_games % lanes else 0) for i in range(lanes)]
+        # a game budget is split like the slots (each lane stops starting games at its share)
+        self.max_games = kw.pop("max_games", None)
+        budgets = [None] * lanes if self.max_games is None else \
+            [self.max_games // lanes + (1 if i < self.max_games % lanes else 0) for i in range(lanes)]
         self.streams = [torch.cuda.Stream(device=self.device) for _ in range(lanes)]
         self.lanes = []
         off = 0
         for i, (n, st) in enumerate(zip(sizes, self.streams)):
             with torch.cuda.stream(st):
                 self.lanes.append(SelfPlayEngine(game, network, n_games=n, seed=seed, subsequence0=subsequence0 + 2 * off,
-                                                 device=self.device, **kw))
+                                                 device=self.device, max_games=budgets[i], **kw))
             off += n
         torch.cuda.synchronize(self.device)
         if lanes > 1 and pack:
@@ -414,6 +419,14 @@ class LanedEngine:
             with torch.cuda.stream(st):
                 out.append(fn(e))
         return out
+
+    def _lanes_wait_caller(self):
+        """Order the lanes' next work after everything the caller queued on its own stream (trainer
+        steps reading the replay ring the lanes append to, optimizer updates of the weights that
+        refresh_network packs): the lanes never run ahead of the caller's stream."""
+        for st in self.streams:
+            if st is not None:
+                st.wait_stream(torch.cuda.current_stream(self.device))
 
     @property
     def positions(self):
@@ -440,12 +453,17 @@ class LanedEngine:
             self.select_timer = self.nn_timer = self.tower_timer = None
 
     def refresh_network(self):
+        self._lanes_wait_caller()
         self._each(lambda e: e.refresh_network())
 
     def ply(self, on_moves=None, refill=True):
         """One move of every active game of every lane. Returns (#games finished, #records exported)."""
-        if not all(e._device_count_ok() for e in self.lanes):
-            res = [(e.ply(on_moves, refill)) for e in self.lanes]
+        self._lanes_wait_caller()
+        if not all(e._device_count_ok() for e in self.lanes):  # host-synchronised evaluators: lane by lane
+            res = []
+            for i, (e, st) in enumerate(zip(self.lanes, self.streams)):
+                with torch.cuda.stream(st):
+                    res.append(e.ply(on_moves, refill, game_offset=i * self.GAME_ID_STRIDE))
         else:
             self._each(lambda e: e._ply_begin())
             for _ in range(self.iterations):
@@ -472,10 +490,13 @@ class LanedEngine:
                 break
             if seconds is not None and time.time() - t0 >= seconds:
                 break
+            if self.max_games is not None and self.games_done >= self.max_games:
+                break
         return dict(plies=n, seconds=time.time() - t0, games=self.games_done, positions=self.positions)
 
     def play_games(self, n, on_moves=None, on_ply=None):
         """As SelfPlayEngine.play_games, the n games split over the lanes."""
+        self._lanes_wait_caller()
         k = len(self.lanes)
         parts = [n // k + (1 if i < n % k else 0) for i in range(k)]
         targets = []
