@@ -18,9 +18,18 @@ def main(path, out):
     rows = []
     for d in disp.values():
         cyc = d["GRBM_GUI_ACTIVE"] / 8
-        rows.append(dict(ns=d["ns"], clock_ghz=cyc / d["ns"],
-                         mfma_busy_frac=d["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * SIMDS),
-                         mfma_insts=d["SQ_INSTS_MFMA"]))
+        row = dict(ns=d["ns"], clock_ghz=cyc / d["ns"],
+                   mfma_busy_frac=d["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * SIMDS))
+        if "SQ_INSTS_MFMA" in d:
+            row["mfma_insts"] = d["SQ_INSTS_MFMA"]
+        if "SQ_WAVE_CYCLES" in d:  # disjoint split of wave cycles (MI355X_MICROARCH.md PMC slots)
+            for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_ANY"):
+                if k in d:
+                    row[k.lower()[3:] + "_frac"] = d[k] / d["SQ_WAVE_CYCLES"]
+        if "SQ_LDS_IDX_ACTIVE" in d:
+            row["lds_bank_conflict_frac"] = d.get("SQ_LDS_BANK_CONFLICT", 0.0) / max(d["SQ_LDS_IDX_ACTIVE"], 1.0)
+            row["lds_active_frac"] = d["SQ_LDS_IDX_ACTIVE"] / (cyc * 256)
+        rows.append(row)
     rows = rows[2:] or rows  # skip warm-up dispatches
     n = len(rows)
     res = {k: sum(r[k] for r in rows) / n for k in rows[0]}
