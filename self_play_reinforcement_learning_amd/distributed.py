@@ -43,6 +43,8 @@ def init_from_env(backend=None):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         kw = {}
+        if os.environ.get("SPMCTS_DIST_INIT"):  # e.g. file:///tmp/x (tests: no TCP port to race for)
+            kw["init_method"] = os.environ["SPMCTS_DIST_INIT"]
         if backend == "nccl":
             torch.cuda.set_device(local)
             kw["device_id"] = torch.device("cuda", local)

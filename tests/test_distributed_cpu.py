@@ -1,7 +1,7 @@
 """CPU: the multi-GPU exchange steps (episode-stat all_reduce, Move gather to rank 0,
 weight broadcast) with torch.distributed gloo, world size 2."""
 import os
-import socket
+import tempfile
 
 import pytest
 import torch
@@ -11,11 +11,9 @@ from self_play_reinforcement_learning_amd import distributed as D
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """A rendezvous for one test: a fresh file store (SPMCTS_DIST_INIT), so concurrent or
+    back-to-back tests never race for a TCP port."""
+    return tempfile.mkdtemp(prefix="spmcts_dist_") + "/store"
 
 
 def _moves(rank, n):
@@ -32,7 +30,7 @@ def _moves(rank, n):
 
 def _worker(rank, world, port, q):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
-                      MASTER_PORT=str(port))
+                      SPMCTS_DIST_INIT="file://" + port)
     D.init_from_env(backend="gloo")
     stats = D.all_reduce_stats([rank + 1, 10 * rank, 1, 0, 0, 0, 1, 0])
     got = D.gather_moves(_moves(rank, 3 + 2 * rank), 42, 7)
@@ -87,7 +85,7 @@ def _loop_worker(rank, world, port, q):
     from self_play_reinforcement_learning_amd.engine import SelfPlayEngine
 
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
-                      MASTER_PORT=str(port))
+                      SPMCTS_DIST_INIT="file://" + port)
     D.init_from_env(backend="gloo")
     eng = _FakeEngine(rate=rank + 1)
     gathered = []
@@ -146,7 +144,7 @@ def _laned_worker(rank, world, port, q):
     from self_play_reinforcement_learning_amd.engine import LanedEngine
 
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
-                      MASTER_PORT=str(port))
+                      SPMCTS_DIST_INIT="file://" + port)
     D.init_from_env(backend="gloo")
     eng = LanedEngine.__new__(LanedEngine)  # lanes without a GPU: no streams, fake arenas
     eng.lanes = [_FakeLane(rate=rank + 1), _FakeLane(rate=1)]
