@@ -58,13 +58,13 @@ def head_linear_flops(W, H, A, filter_factor):
 def select_bytes(sims, levels, A=7):
     """Algorithmic HBM bytes moved by k_select.
 
-    Per scored level: the child block (A x {n i32, w f64, p f32, child i32}) + vmask + the
-    node's child index = 20A + 8.  Per simulation: tree header (active id, root id/board/
-    player, noise flag, A noise doubles, root n/w) + Philox state load/store = 86 + 8A + 128,
-    leaf record writes (16 per path entry + 38).
+    Per scored level: the child block (A x {n i32, w f64, p f32, child i32}) + vmask = 20A + 4
+    (the next level's child-block index comes with the block).  Per simulation: tree header
+    (active id, root id/board/player, noise flag, A noise doubles, root n/w/child index) +
+    Philox state load/store = 90 + 8A + 128, leaf record writes (16 per path entry + 38).
     """
-    per_level = 20 * A + 8 + 16
-    per_sim = 86 + 8 * A + 128 + 38
+    per_level = 20 * A + 4 + 16
+    per_sim = 90 + 8 * A + 128 + 38
     return levels * per_level + sims * per_sim
 
 

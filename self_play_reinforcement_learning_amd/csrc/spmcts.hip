@@ -368,6 +368,9 @@ __global__ __launch_bounds__(64) void k_select(View v, int n_active) {
 
   int node_n = v.bn[nb + node];
   double node_w = v.bw[nb + node];
+  // the node's child block: read for the root; below it, the child entry read with the parent's
+  // block already holds it (one dependent global load per level instead of two)
+  int cb = v.bc[nb + node];
   int depth = 0;
   for (;;) {
     if (lane == 0) {
@@ -375,7 +378,6 @@ __global__ __launch_bounds__(64) void k_select(View v, int n_active) {
       s_n[grp][depth] = node_n;
       s_w[grp][depth] = node_w;
     }
-    const int cb = v.bc[nb + node];
     if (cb < 0) {  // an expanded node is required here
       if (lane == 0) set_err(v, SPMCTS_ERR_STATE);
       return;
@@ -468,6 +470,7 @@ __global__ __launch_bounds__(64) void k_select(View v, int n_active) {
     node = child;
     node_n = cn_a;
     node_w = cw_a;
+    cb = cc_a;
     player = -player;
     ++depth;
     if (depth >= G::MAXD) {
