@@ -24,8 +24,14 @@
 #include <stdlib.h>
 
 #include "spmcts.h"
+#include "tower_edge.h"
 
 namespace tower {
+
+// edge-tile layout tables (tower_edge.h): row -> (board, x, y) packed, (board, x, y) -> row
+constexpr uint16_t kEdgeRow[256] = EDGE_ROW_INIT;
+constexpr uint16_t kEdgeCellRow[6 * 7 * 6] = EDGE_CELL_ROW_INIT;
+
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -36,7 +42,7 @@ typedef short i16x2 __attribute__((ext_vector_type(2)));
 
 
 template <int C_, int ROWS_, int W_, int H_, int CG_ = 2, int WAVES_ = 4, int ABL_ = 0, int DEPTH_ = 4, int OCC_ = 1,
-          bool XMAJ_ = false>
+          bool XMAJ_ = false, bool EDGE_ = false>
 struct Cfg {
   static constexpr int OCC = OCC_;  // resident workgroups per CU the register budget is sized for
   static constexpr int DEPTH = DEPTH_;  // weight-fragment prefetch distance (k-steps)
@@ -63,13 +69,20 @@ struct Cfg {
   static constexpr int NT = ROWS / 32 / MG;  // 32-cell tiles per wave
   static constexpr int MT = C / 32 / CG;     // 32-channel tiles per wave
   static constexpr int BUF = (ROWS + NZ) * RS;
-  static constexpr int LDS = 2 * BUF;
+  // Edge tiles (EDGE, a column-major-tile variant): rows ordered by tower_edge.h so that whole cell
+  // tiles hold only x = 0, y = 0, x = W-1 or y = H-1 cells; 12 of the workgroup's 72 (tile, tap)
+  // pairs read zero padding only and are skipped.  Neighbours are no longer affine row offsets:
+  // a 9 x ROWS table of neighbour rows (zero rows for off-board) sits in LDS after the buffers.
+  static constexpr bool EDGE = EDGE_ && XMAJ_;
+  static constexpr int TAB = EDGE ? 9 * ROWS * 2 : 0;
+  static constexpr int LDS = 2 * BUF + TAB;
   static constexpr int HEAD = C / 2;  // policy filter_factor | value filter_factor channels (filter_factor = C/4)
   static constexpr int HCT = HEAD / 32;  // head channel tiles
   static_assert(MT >= 1 && NT >= 1 && MT * NT <= 8, "tile plan: at most 8 accumulator tiles per wave");
   static_assert(CG * MG == WAVES, "wave plan");
   static_assert(BOARDS >= 1, "board larger than a tile");
   static_assert(LDS <= 163840, "LDS budget");
+  static_assert(!EDGE_ || (W == 7 && H == 6 && ROWS == 256 && BOARDS == 6 && MG == 2), "edge layout: 6 Connect4 boards");
   // Row layout of the tile.  Board-major (default): row = board * CELLS + x * H + y.  Column-major
   // across boards (XMAJ): row = x * (BOARDS * H) + board * H + y, so each board column x of all the
   // tile's boards is BOARDS*H consecutive rows: with 6 boards (36 rows per column) cell tile 0 lies
@@ -79,9 +92,21 @@ struct Cfg {
   static constexpr bool XMAJ = XMAJ_;
   static constexpr int DX = XMAJ ? BOARDS * H : H;
   // (board, x, y) of a row < VROWS
-  __host__ __device__ static constexpr int row_board(int row) { return XMAJ ? (row / H) % BOARDS : row / CELLS; }
-  __host__ __device__ static constexpr int row_x(int row) { return XMAJ ? row / (BOARDS * H) : (row % CELLS) / H; }
-  __host__ __device__ static constexpr int row_y(int row) { return row % H; }
+  __host__ __device__ static constexpr int row_board(int row) {
+    return EDGE ? kEdgeRow[row] >> 6 : XMAJ ? (row / H) % BOARDS : row / CELLS;
+  }
+  __host__ __device__ static constexpr int row_x(int row) {
+    return EDGE ? (kEdgeRow[row] >> 3) & 7 : XMAJ ? row / (BOARDS * H) : (row % CELLS) / H;
+  }
+  __host__ __device__ static constexpr int row_y(int row) { return EDGE ? kEdgeRow[row] & 7 : row % H; }
+  // does any on-board row of cell tile T have an on-board neighbour for `tap`?
+  __host__ __device__ static constexpr bool tile_tap_live(int T, int tap) {
+    for (int r = T * 32; r < T * 32 + 32 && r < VROWS; ++r) {
+      const int nx = row_x(r) + tap / 3 - 1, ny = row_y(r) + tap % 3 - 1;
+      if (nx >= 0 && nx < W && ny >= 0 && ny < H) return true;
+    }
+    return false;
+  }
   __host__ __device__ static constexpr int row_cell(int row) { return row_x(row) * H + row_y(row); }
   // does any on-board row of 32-row cell tile T have an on-board neighbour column x + dx?
   __host__ __device__ static constexpr bool tile_dx_live(int T, int dx) {
@@ -120,6 +145,7 @@ struct Nbr {
   int base[K::NT];
   int rowi[K::NT];
   uint32_t mask[K::NT];
+  const uint16_t *tab;  // Cfg::EDGE: LDS neighbour-row table [9][ROWS]
   __device__ __forceinline__ void init(int r, int mg) {
 #pragma unroll
     for (int t = 0; t < K::NT; ++t) {
@@ -141,6 +167,7 @@ struct Nbr {
   // byte offset of the source row of tile t for `tap` (the zero row when off the board); a
   // branch-free select (hipcc otherwise emits an exec-mask branch per tile and tap)
   __device__ __forceinline__ int off(int t, int tap) const {
+    if constexpr (K::EDGE) return (int)tab[tap * K::ROWS + rowi[t]] * K::RS;
     const int dr = (tap / 3 - 1) * K::DX + (tap % 3 - 1);
     const int on = base[t] + dr * K::RS;
     const int zero = (K::ZROW + ((rowi[t] + dr) & (K::NZ - 1))) * K::RS;
@@ -497,7 +524,90 @@ struct XLive {
   static constexpr uint32_t LIVE[3] = {mask(0), mask(1), mask(2)};
   // tiles not live in group 0 miss the zero-start step 0: their accumulators start at zero
   static constexpr uint32_t ZPRE = ALL & ~LIVE[0];
+  // per-tap live tiles (Cfg::EDGE: a tile can be dead for taps of one dy as well)
+  static constexpr uint32_t lt(int tap) {
+    uint32_t m = 0;
+    for (int t = 0; t < K::NT; ++t)
+      if (K::tile_tap_live(MG_ * K::NT + t, tap)) m |= 1u << t;
+    return m;
+  }
+  static constexpr uint32_t ZPRE_T = ALL & ~lt(0);
 };
+
+// One tap of a column-major / edge-tile layer with per-tap live tiles (Cfg::EDGE): conv_group_x's
+// pipeline for one tap; the B fragments of the next tap are read for its own live tiles.
+template <class K, int KK, int DEPTH, int MG_, int TAP>
+__device__ __forceinline__ void conv_tap_x(const char *src, const Nbr<K> &nb, f32x16 (&acc)[K::MT][K::NT],
+                                           bf16x8 (&bc)[K::NT], bf16x8 (&bn)[K::NT], int (&off_cur)[K::NT],
+                                           int (&off_nxt)[K::NT], bf16x8 (&a)[DEPTH][K::MT], int hoff,
+                                           const WBuf &wb, uint32_t wl_off, uint32_t wn_off, int wn_steps) {
+  using X = XLive<K, MG_>;
+  constexpr uint32_t MSTRIDE = 9u * KK * 1024u;
+  constexpr int STEPS = 9 * KK;
+  constexpr uint32_t LV = X::lt(TAP);
+  constexpr uint32_t LVN = TAP < 8 ? X::lt(TAP < 8 ? TAP + 1 : 8) : 0u;
+  constexpr int NTA = (int)X::popc(LV);
+  static_assert(NTA >= 1 && K::MT * NTA >= NTA + K::MT, "schedule: enough MFMAs for the loads");
+  if constexpr (TAP < 8) {
+#pragma unroll
+    for (int t = 0; t < K::NT; ++t)
+      if ((LVN >> t) & 1u) off_nxt[t] = nb.off(t, TAP + 1) + hoff;
+  }
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) {
+    const int s = TAP * KK + kk;
+    if (kk + 1 < KK) {
+#pragma unroll
+      for (int t = 0; t < K::NT; ++t)
+        if ((LV >> t) & 1u) bn[t] = lds_b128(src + off_cur[t] + (kk + 1) * 32);
+    } else if (TAP < 8) {
+#pragma unroll
+      for (int t = 0; t < K::NT; ++t)
+        if ((LVN >> t) & 1u) bn[t] = lds_b128(src + off_nxt[t]);
+    }
+    const int slot = kk % DEPTH;
+    bf16x8 acur[K::MT];
+#pragma unroll
+    for (int m = 0; m < K::MT; ++m) acur[m] = a[slot][m];
+    const int sn = s + DEPTH;
+    if (sn < STEPS) {
+#pragma unroll
+      for (int m = 0; m < K::MT; ++m) a[slot][m] = wb.load(wl_off + m * MSTRIDE + (uint32_t)sn * 1024u);
+    } else if (sn - STEPS < wn_steps) {
+#pragma unroll
+      for (int m = 0; m < K::MT; ++m) a[slot][m] = wb.load(wn_off + m * MSTRIDE + (uint32_t)(sn - STEPS) * 1024u);
+    }
+    if (TAP == 0 && kk == 0) {
+#pragma unroll
+      for (int t = 0; t < K::NT; ++t)
+#pragma unroll
+        for (int m = 0; m < K::MT; ++m)
+          if ((LV >> t) & 1u) acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[m], bc[t], f32x16{}, 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int t = 0; t < K::NT; ++t)
+#pragma unroll
+        for (int m = 0; m < K::MT; ++m)
+          if ((LV >> t) & 1u) acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[m], bc[t], acc[m][t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NTA; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+    }
+#pragma unroll
+    for (int i = 0; i < K::MT; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, K::MT * NTA - NTA - K::MT, 0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < K::NT; ++t) bc[t] = bn[t];
+  }
+#pragma unroll
+  for (int t = 0; t < K::NT; ++t) off_cur[t] = off_nxt[t];
+}
 
 template <class K, int KK, int DEPTH, int MG_, int G>
 __device__ __forceinline__ void conv_group_x(const char *src, const Nbr<K> &nb, f32x16 (&acc)[K::MT][K::NT],
@@ -596,15 +706,22 @@ __device__ __forceinline__ void conv_layer_x(const char *src, char *dst, const N
   for (int t = 0; t < K::NT; ++t)
 #pragma unroll
     for (int m = 0; m < K::MT; ++m)
-      if ((X::ZPRE >> t) & 1u) acc[m][t] = f32x16{};
+      if (((K::EDGE ? X::ZPRE_T : X::ZPRE) >> t) & 1u) acc[m][t] = f32x16{};
   int off_cur[K::NT], off_nxt[K::NT];
   bf16x8 bc[K::NT], bn[K::NT];
 #pragma unroll
   for (int t = 0; t < K::NT; ++t)
-    if ((X::LIVE[0] >> t) & 1u) {
+    if (((K::EDGE ? X::lt(0) : X::LIVE[0]) >> t) & 1u) {
       off_cur[t] = nb.off(t, 0) + hoff;
       bc[t] = lds_b128(src + off_cur[t]);
     }
+  if constexpr (K::EDGE) {
+#define TAPX(T) conv_tap_x<K, KK, DEPTH, MG_, T>(src, nb, acc, bc, bn, off_cur, off_nxt, a, hoff, wb, wl_off, wn_off, wn_steps)
+    TAPX(0); TAPX(1); TAPX(2); TAPX(3); TAPX(4); TAPX(5); TAPX(6); TAPX(7); TAPX(8);
+#undef TAPX
+    acc_store_bias_relu_pre<K, RESID>(acc, dst, bv, wave, lane);
+    return;
+  }
   conv_group_x<K, KK, DEPTH, MG_, 0>(src, nb, acc, bc, bn, off_cur, off_nxt, a, hoff, wb, wl_off, wn_off, wn_steps);
   conv_group_x<K, KK, DEPTH, MG_, 1>(src, nb, acc, bc, bn, off_cur, off_nxt, a, hoff, wb, wl_off, wn_off, wn_steps);
   conv_group_x<K, KK, DEPTH, MG_, 2>(src, nb, acc, bc, bn, off_cur, off_nxt, a, hoff, wb, wl_off, wn_off, wn_steps);
@@ -710,6 +827,19 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
   for (int i = tid; i < K::NZ * K::RS / 4; i += K::THREADS) {
     ((uint32_t *)(X + K::ZROW * K::RS))[i] = 0u;
     ((uint32_t *)(Y + K::ZROW * K::RS))[i] = 0u;
+  }
+  if constexpr (K::EDGE) {
+    uint16_t *tab = (uint16_t *)(smem + 2 * K::BUF);
+    for (int i = tid; i < 9 * K::ROWS; i += K::THREADS) {
+      const int tap = i / K::ROWS, row = i % K::ROWS;
+      int nr = K::ZROW + ((row + tap) & (K::NZ - 1));  // off the board: a zero row, spread over banks
+      if (row < K::VROWS) {
+        const int b = K::row_board(row), x = K::row_x(row) + tap / 3 - 1, y = K::row_y(row) + tap % 3 - 1;
+        if (x >= 0 && x < K::W && y >= 0 && y < K::H) nr = kEdgeCellRow[(b * K::W + x) * K::H + y];
+      }
+      tab[i] = (uint16_t)nr;
+    }
+    nb.tab = tab;
   }
   for (int row = tid; row < K::ROWS; row += K::THREADS) {
     const int board = board0 + K::row_board(row);
@@ -1072,7 +1202,7 @@ extern "C" int spmcts_tower_forward_dev(int32_t width, int32_t height, int32_t c
   if (max_batch == 0) return 0;
   const bool pack = (flags & SPMCTS_TOWER_PACK) != 0;
   if (width == 7 && height == 6 && channels == 128)
-    return launch_dyn<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true>, Cfg<128, 192, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(planes_dev, count_dev, max_batch, n_blocks,
+    return launch_dyn<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true, true>, Cfg<128, 192, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(planes_dev, count_dev, max_batch, n_blocks,
                                                                       weights_dev, bias_dev, features_dev, pack, s);
   if (width == 7 && height == 6 && channels == 256)
     return launch_dyn<Cfg<256, 128, 7, 6, 4>, Cfg<256, 128, 7, 6, 4>, Cfg<256, 128, 7, 6, 4>>(planes_dev, count_dev, max_batch, n_blocks,
@@ -1107,8 +1237,9 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
       ABLATE(256) ABLATE(2048) ABLATE(32768)
 #undef ABLATE
       case 10: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);  // two tile sizes only
+      case 15: return launch_split<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true>, Cfg<128, 192, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);  // column-major tiles without edge rows
       case 11: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 192, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);  // board-major full tiles
-      default: return launch_split<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true>, Cfg<128, 192, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      default: return launch_split<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true, true>, Cfg<128, 192, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
     }
   }
   if (width == 7 && height == 6 && channels == 256)
