@@ -1,37 +1,150 @@
-import itertools
-G=[list(range(0,4))+list(range(12,16))+list(range(20,28)), list(range(4,12))+list(range(16,20))+list(range(28,32))]
-G=G+[[l+32 for l in g] for g in G]
-RS=272; ZROW=256
-def build(order_C, order_A, order_D, order_B, order_E):
-    rows=[None]*256
-    # A: x=0 cells
-    A=[(b,0,y) for b in range(6) for y in range(1,5)]
-    A=sorted(A,key=order_A)+[(b,0,0) for b in range(4)]+[(b,0,5) for b in range(4)]
-    B=sorted([(b,x,0) for b in range(6) for x in range(1,6)],key=order_B)+[(4,0,0),(5,0,0)]
-    C=sorted([(b,x,y) for b in range(6) for x in range(1,6) for y in range(1,5)],key=order_C)+[(4,0,5),(5,0,5),(4,6,0),(5,6,0),(4,6,5),(5,6,5),(5,4,5),(5,5,5)]
-    D=sorted([(b,6,y) for b in range(6) for y in range(1,5)],key=order_D)+[(b,6,0) for b in range(4)]+[(b,6,5) for b in range(4)]
-    E=sorted([(b,x,5) for b in range(5) for x in range(1,6)]+[(5,1,5),(5,2,5),(5,3,5)],key=order_E)
-    allc=A+B+C+D+E
-    assert len(allc)==252 and len(set(allc))==252
-    for i,c in enumerate(allc): rows[i]=c
-    inv={c:i for i,c in enumerate(allc)}
-    return rows,inv
-def cost(rows,inv,zsel):
-    tot=0;n=0
+"""Edge-tile row layout of a 6-board Connect4 tile (tower.hip Cfg::EDGE) and its LDS bank model.
+
+Writes self_play_reinforcement_learning_amd/csrc/tower_edge.h: EDGE_ROW (row -> board/x/y),
+EDGE_CELL_ROW (cell -> row) and EDGE_NBR ([tap][row] -> source row, zero rows for off-board).
+
+Constraints: rows 0-31 hold only x = 0 cells, 32-63 only y = 0, 192-223 only x = 6, 224-251 only
+y = 5 (+ the 4 padding rows), so those tiles' dx = -1 / dy = -1 / dx = +1 / dy = +1 taps read
+zero padding only.  Within those classes the order is free: it is chosen by a local search that
+minimises the modelled ds_read_b128 bank sharing of the B-fragment reads (MI355X_MICROARCH.md:
+16-lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, bank = (addr / 4) mod 64, 272-B rows = a
+4-bank shift per row), and each off-board neighbour gets the zero row (one of 16) whose bank
+position no other lane of its group uses.
+    python scripts/edge_layout_model.py [--iters N] [--seed S]
+"""
+import argparse
+import os
+import random
+
+GROUPS = [list(range(0, 4)) + list(range(12, 16)) + list(range(20, 28)),
+          list(range(4, 12)) + list(range(16, 20)) + list(range(28, 32))]
+ROWS, VROWS, ZROW, NZ = 256, 252, 256, 16
+W, H, B = 7, 6, 6
+
+
+def classes():
+    """The five row regions: (first row, cells allowed there)."""
+    corners_x0 = [(b, 0, 0) for b in range(4)] + [(b, 0, 5) for b in range(4)]
+    corners_x6 = [(b, 6, 0) for b in range(4)] + [(b, 6, 5) for b in range(4)]
+    A = [(b, 0, y) for b in range(6) for y in range(1, 5)] + corners_x0
+    Bc = [(b, x, 0) for b in range(6) for x in range(1, 6)] + [(4, 0, 0), (5, 0, 0)]
+    C = ([(b, x, y) for b in range(6) for x in range(1, 6) for y in range(1, 5)]
+         + [(4, 0, 5), (5, 0, 5), (4, 6, 0), (5, 6, 0), (4, 6, 5), (5, 6, 5), (5, 4, 5), (5, 5, 5)])
+    D = [(b, 6, y) for b in range(6) for y in range(1, 5)] + corners_x6
+    E = [(b, x, 5) for b in range(5) for x in range(1, 6)] + [(5, 1, 5), (5, 2, 5), (5, 3, 5)]
+    return [(0, A), (32, Bc), (64, C), (192, D), (224, E)]
+
+
+def initial():
+    key = lambda c: (c[2], c[1], c[0])  # boards fastest
+    rows = [None] * ROWS
+    for start, cells in classes():
+        for i, c in enumerate(sorted(cells, key=key)):
+            rows[start + i] = c
+    return rows
+
+
+def on_board(c, tap):
+    return 0 <= c[1] + tap // 3 - 1 < W and 0 <= c[2] + tap % 3 - 1 < H
+
+
+def group_cost(rows, inv, T, tap, g):
+    pos = {}
+    for l in g:
+        c = rows[T * 32 + l]
+        if c is not None and on_board(c, tap):
+            p = inv[(c[0], c[1] + tap // 3 - 1, c[2] + tap % 3 - 1)] % 16
+            pos[p] = pos.get(p, 0) + 1
+    return max(pos.values()) if pos else 1
+
+
+def live(rows, T, tap):
+    return any(rows[r] is not None and on_board(rows[r], tap) for r in range(T * 32, T * 32 + 32))
+
+
+def total(rows):
+    inv = {c: r for r, c in enumerate(rows) if c is not None}
+    return sum(group_cost(rows, inv, T, tap, g) for T in range(8) for tap in range(9) if live(rows, T, tap)
+               for g in GROUPS)
+
+
+def zero_rows(rows):
+    """EDGE_NBR[tap][row]: on-board neighbour row, else a zero row at a bank position unused by
+    the on-board lanes of the row's 16-lane group."""
+    inv = {c: r for r, c in enumerate(rows) if c is not None}
+    nbr = [[0] * ROWS for _ in range(9)]
     for T in range(8):
         for tap in range(9):
-            dx,dy=tap//3-1,tap%3-1
-            rr=[rows[r] for r in range(T*32,T*32+32)]
-            if not any(c and 0<=c[1]+dx<7 and 0<=c[2]+dy<6 for c in rr): continue
-            for kk in range(8):
-                for g in G:
-                    banks={}
-                    for l in g:
-                        r=T*32+(l&31); h=l>>5; c=rows[r]
-                        if c and 0<=c[1]+dx<7 and 0<=c[2]+dy<6: nr=inv[(c[0],c[1]+dx,c[2]+dy)]
-                        else: nr=ZROW+zsel(r,tap)
-                        a=nr*RS+kk*32+16*h
-                        for k in range(4):
-                            banks.setdefault(((a//4)+k)%64,set()).add(a//4+k)
-                    tot+=max(len(s) for s in banks.values()); n+=1
-    return tot/n
+            for g in GROUPS:
+                used, off = set(), []
+                for l in g:
+                    r = T * 32 + l
+                    c = rows[r]
+                    if c is not None and on_board(c, tap):
+                        n = inv[(c[0], c[1] + tap // 3 - 1, c[2] + tap % 3 - 1)]
+                        nbr[tap][r] = n
+                        used.add(n % 16)
+                    else:
+                        off.append(r)
+                free = [p for p in range(16) if p not in used] + [p for p in range(16) if p in used]
+                for i, r in enumerate(off):
+                    nbr[tap][r] = ZROW + free[i % 16]
+    return nbr
+
+
+def anneal(rows, iters, seed):
+    rnd = random.Random(seed)
+    regions = [(s, s + len(c)) for s, c in classes()]
+    cur = total(rows)
+    for it in range(iters):
+        lo, hi = rnd.choice(regions)
+        i, j = rnd.randrange(lo, hi), rnd.randrange(lo, hi)
+        if i == j:
+            continue
+        rows[i], rows[j] = rows[j], rows[i]
+        c = total(rows)
+        if c <= cur:
+            cur = c
+        else:
+            rows[i], rows[j] = rows[j], rows[i]
+    return rows, cur
+
+
+def write_header(rows, nbr, path, note):
+    enc = [255 if c is None else c[0] * 64 + c[1] * 8 + c[2] for c in rows]
+    inv = {c: r for r, c in enumerate(rows) if c is not None}
+    cell_row = [inv[(b, x, y)] for b in range(B) for x in range(W) for y in range(H)]
+    flat = [v for tap in range(9) for v in nbr[tap]]
+
+    def arr(name, v):
+        body = ", \\\n".join("    " + ", ".join(str(x) for x in v[i:i + 24]) for i in range(0, len(v), 24))
+        return "#define %s_INIT { \\\n%s }\n" % (name, body)
+
+    hdr = ("// tower_edge.h — generated by scripts/edge_layout_model.py (%s).\n"
+           "// Edge-tile row layout of a 6-board Connect4 tile (Cfg::EDGE): row r holds cell (b, x, y) =\n"
+           "// (v >> 6, (v >> 3) & 7, v & 7) of v = EDGE_ROW[r] (255 = padding row); EDGE_CELL_ROW[(b * 7 + x) * 6 + y]\n"
+           "// is its row; EDGE_NBR[tap * 256 + r] the source row of tap (dx, dy) = (tap / 3 - 1, tap %% 3 - 1),\n"
+           "// a zero row (256 + i) off the board.  Tiles 0 / 1 / 6 / 7 hold only x = 0 / y = 0 / x = 6 /\n"
+           "// y = 5 cells, so their dx = -1 / dy = -1 / dx = +1 / dy = +1 taps read zero padding only.\n"
+           "#pragma once\n" % note) + arr("EDGE_ROW", enc) + arr("EDGE_CELL_ROW", cell_row) + arr("EDGE_NBR", flat)
+    open(path, "w").write(hdr)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=3000)
+    ap.add_argument("--seed", type=int, default=1)
+    args = ap.parse_args()
+    rows = initial()
+    c0 = total(rows)
+    rows, c1 = anneal(rows, args.iters, args.seed)
+    n = sum(1 for T in range(8) for tap in range(9) if live(rows, T, tap)) * len(GROUPS)
+    note = "modelled bank sharing %.3f -> %.3f per 16-lane read, %d swaps tried" % (c0 / n, c1 / n, args.iters)
+    print(note)
+    here = os.path.dirname(os.path.abspath(__file__))
+    write_header(rows, zero_rows(rows), os.path.join(here, "..", "self_play_reinforcement_learning_amd", "csrc",
+                                                     "tower_edge.h"), note)
+
+
+if __name__ == "__main__":
+    main()

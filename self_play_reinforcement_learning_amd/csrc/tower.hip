@@ -31,6 +31,9 @@ namespace tower {
 // edge-tile layout tables (tower_edge.h): row -> (board, x, y) packed, (board, x, y) -> row
 constexpr uint16_t kEdgeRow[256] = EDGE_ROW_INIT;
 constexpr uint16_t kEdgeCellRow[6 * 7 * 6] = EDGE_CELL_ROW_INIT;
+// [tap][row] source row (zero rows off the board, at bank positions no on-board lane of the
+// 16-lane read group uses)
+constexpr uint16_t kEdgeNbr[9 * 256] = EDGE_NBR_INIT;
 
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -830,15 +833,8 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
   }
   if constexpr (K::EDGE) {
     uint16_t *tab = (uint16_t *)(smem + 2 * K::BUF);
-    for (int i = tid; i < 9 * K::ROWS; i += K::THREADS) {
-      const int tap = i / K::ROWS, row = i % K::ROWS;
-      int nr = K::ZROW + ((row + tap) & (K::NZ - 1));  // off the board: a zero row, spread over banks
-      if (row < K::VROWS) {
-        const int b = K::row_board(row), x = K::row_x(row) + tap / 3 - 1, y = K::row_y(row) + tap % 3 - 1;
-        if (x >= 0 && x < K::W && y >= 0 && y < K::H) nr = kEdgeCellRow[(b * K::W + x) * K::H + y];
-      }
-      tab[i] = (uint16_t)nr;
-    }
+    static_assert(K::ROWS == 256 && K::ZROW == 256, "EDGE_NBR is laid out for 256-row tiles");
+    for (int i = tid; i < 9 * K::ROWS; i += K::THREADS) tab[i] = kEdgeNbr[i];
     nb.tab = tab;
   }
   for (int row = tid; row < K::ROWS; row += K::THREADS) {
