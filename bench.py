@@ -137,6 +137,9 @@ def main():
                     help="arenas per GPU on their own HIP streams (engine.LanedEngine); 1 = one arena")
     ap.add_argument("--no-pack", action="store_true",
                     help="lanes > 1: keep round-aligned tower tiles (no SPMCTS_TOWER_PACK)")
+    ap.add_argument("--search-threads", type=int, default=1,
+                    help="sims in flight per tree with virtual loss (the reference's thread_count search, "
+                         "mcts.py:328-331); 1 = sequential search (bit-exact to the reference's sequential mode)")
     args = ap.parse_args()
     arena_mode = args.mode == "arena"
 
@@ -164,7 +167,7 @@ def main():
         torch.manual_seed(1)
         opponent = ResidualTower(7, 6, 7, num_blocks=args.blocks, filter_factor=args.filter_factor).to(dev).eval()
     kw = dict(iterations=args.sims, seed=1234 + rank, device=dev, bucket=args.bucket, opponent=opponent,
-              evaluate=arena_mode, record=not arena_mode)
+              evaluate=arena_mode, record=not arena_mode, search_threads=args.search_threads)
     if args.lanes > 1:
         eng = LanedEngine("connect4", net, n_games=args.games, lanes=args.lanes, pack=not args.no_pack, **kw)
     else:
@@ -270,6 +273,7 @@ def main():
             "net": f"ResidualTower(filter_factor={args.filter_factor}, num_blocks={args.blocks})",
             "parallelism": f"dp{world}",
             "lanes_per_gpu": max(1, args.lanes),
+            "search_threads": args.search_threads,
         },
         "roofline": {
             "kernel": f"tower::k_tower_dyn (fused ResNet-{4 * args.filter_factor}x{args.blocks} trunk, bf16 MFMA)",

@@ -82,7 +82,9 @@ typedef struct spmcts_config {
   int32_t leaf_format;     /* enum spmcts_leaf_format                                         */
   int32_t leaf_layout;     /* enum spmcts_layout (planes only)                                */
   int32_t compact;         /* 1: leaf rows compacted in tree order; 0: one row per active slot */
-  int32_t reserved0;
+  int32_t search_threads;  /* K simulations in flight per tree with virtual loss (the reference's
+                              thread_count, mcts.py:328-331, :345); 0 or 1 = sequential search.
+                              Leaf rows per select = n_trees * K; K > 1 keeps a per-node vl.  */
   double cpuct;            /* MCNode.cpuct = 4 (mcts.py:25)                                   */
   double x_noise;          /* MCNode.x = 0.25 (mcts.py:25)                                    */
   double alpha;            /* Dirichlet alpha (mcts.py:135)                                   */

@@ -20,6 +20,17 @@ Backup (mcts.py:94-98) recurses to the ORIGINAL game root; the nodes above the
 active root are never read again, so the restatement stops at the active root
 (observationally equivalent).
 
+Threaded mode (`threads=K > 1`, the reference's `thread_count` search when its
+network is an InferenceProxy, mcts.py:154, :328-331): the reference's threads
+interleave nondeterministically, so the restatement fixes one interleaving —
+each step, K search_node calls select (virtual loss += 1 on the nodes they pass,
+pending leaves locked, terminal leaves backed up at once) before any network
+reply; then the K replies are expanded and backed up in call order, each removing
+its path's virtual loss.  This is the interleaving the HIP arena's k_select_vl /
+k_expand_vl implement.  Parity of this mode is anchored on the reference's
+sequential fixtures (K=1 reduces to them) plus this restatement: the reference
+itself cannot produce a deterministic threaded trace.
+
 RNG: every random draw goes through an `rng` object with the reference's call
 order: per search one `dirichlet(alpha, A)`, per descended
 level one `rand(A)`, per move one uniform for `np.random.choice`.
@@ -153,7 +164,7 @@ class Node:
     """MCNode fields (mcts.py:24-47) minus the threading lock (sequential mode)."""
 
     __slots__ = ("n", "w", "p", "x", "cpuct", "player", "valid", "vl", "noise_active", "p_noise",
-                 "children", "state", "v")
+                 "children", "state", "v", "locked")
 
     def __init__(self, p=0.0, player=1, valid=True, x=0.25, cpuct=4):
         self.n = 0
@@ -169,6 +180,7 @@ class Node:
         self.children = ()
         self.state = None
         self.v = None
+        self.locked = False  # threading.Lock held while a threaded search waits for the network
 
     def q(self):  # mcts.py:59-62
         n_eff = self.n + self.vl
@@ -200,7 +212,7 @@ class OracleTree:
     """MCTreeSearch (mcts.py:116-394), sequential mode, inference only."""
 
     def __init__(self, game, network, rng, iterations=100, alpha=1, strong_play=False, cpuct=4, x=0.25,
-                 evaluate=False, root_player=1):
+                 evaluate=False, root_player=1, threads=1):
         self.game = game
         self.env_proto = make_env(game)
         self.A = self.env_proto.n_actions
@@ -212,8 +224,9 @@ class OracleTree:
         self.cpuct = cpuct
         self.x = x
         self.evaluating = evaluate
+        self.threads = max(1, int(threads))
         self.temp_memory = []
-        self.stats = dict(sims=0, nn_evals=0, terminal_leaves=0, depth_sum=0, set_node_expansions=0)
+        self.stats = dict(sims=0, nn_evals=0, terminal_leaves=0, depth_sum=0, set_node_expansions=0, leaks=0)
         self.reset(root_player)
 
     def reset(self, player=1):  # mcts.py:166-174
@@ -237,10 +250,76 @@ class OracleTree:
 
     def search(self):  # mcts.py:323-338
         self._add_noise(self.root)
-        for _ in range(self.iterations):
-            self.search_node()
+        if self.threads > 1:  # mcts.py:328-331
+            done = 0
+            while done < self.iterations:
+                k = min(self.threads, self.iterations - done)
+                pending = [self._select_threaded() for _ in range(k)]
+                for item in pending:
+                    if item is not None:
+                        self._reply_threaded(*item)
+                done += k
+        else:
+            for _ in range(self.iterations):
+                self.search_node()
         for c in self.root.children:
             c.noise_active = False
+
+    def _select_threaded(self):
+        """search_node (mcts.py:340-367) up to the network call; returns the pending leaf or None."""
+        node = self.root
+        path = []
+        depth = 0
+        while True:
+            path.append(node)
+            node.vl += 1
+            scores = [c.select_prob(node) if c.valid and not c.locked else -10000000000 for c in node.children]
+            if all(s < -100000 for s in scores):
+                self.stats["leaks"] += 1
+                return None  # mcts.py:349-354 (the virtual loss stays)
+            action = int(np.argmax(scores + 0.000001 * self.rng.rand(self.A)))
+            child = node.children[action]
+            if child.is_leaf():
+                self.stats["sims"] += 1
+                self.stats["depth_sum"] += depth + 1
+                env = make_env(self.game)
+                env.set_state(node.state.copy())
+                s, r, done, _ = env.step(action, player=node.player)
+                r = r * node.player
+                if done:  # _expand_node's terminal branch: no network call, backup at once
+                    if self.strong_play:
+                        num_steps = np.sum(np.abs(node.state)) + 1
+                        v = (1.18 - (9 * num_steps / 350)) * r
+                    else:
+                        v = r
+                    self.stats["terminal_leaves"] += 1
+                    child.state = s
+                    self._backup_threaded(child, path, v)
+                    return None
+                child.locked = True  # mcts.py:359
+                return child, path, s, env.valid_moves(), node.player
+            node = child
+            depth += 1
+
+    def _reply_threaded(self, child, path, s, valid, parent_player):
+        probs, v = self.network(s, parent_player)  # mcts.py:316
+        self.stats["nn_evals"] += 1
+        child.create_children(probs, valid)
+        child.state = s
+        self._backup_threaded(child, path, v)
+        child.locked = False
+
+    @staticmethod
+    def _backup_threaded(leaf, path, v):  # mcts.py:361-365
+        leaf.n += 1
+        leaf.w += v
+        for a in path:
+            a.n += 1
+            a.w += v
+        leaf.v = v
+        for a in path:
+            a.vl -= 1
+            assert a.vl >= 0
 
     def _add_noise(self, node):  # mcts.py:49-53
         d = self.rng.dirichlet(self.alpha, len(node.children))

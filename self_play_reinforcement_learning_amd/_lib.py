@@ -43,7 +43,7 @@ class Config(ctypes.Structure):
         ("leaf_format", ctypes.c_int32),
         ("leaf_layout", ctypes.c_int32),
         ("compact", ctypes.c_int32),
-        ("reserved0", ctypes.c_int32),
+        ("search_threads", ctypes.c_int32),
         ("cpuct", ctypes.c_double),
         ("x_noise", ctypes.c_double),
         ("alpha", ctypes.c_double),

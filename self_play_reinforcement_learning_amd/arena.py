@@ -50,7 +50,7 @@ class Arena:
 
     def __init__(self, game="connect4", n_trees=2, n_games=0, iterations=100, rng="philox", seed=0,
                  subsequence0=0, strong_play=False, evaluate=False, leaf_format="bf16", leaf_layout="nchw",
-                 cpuct=4.0, x_noise=0.25, alpha=1.0, blocks_per_tree=0, device=None):
+                 cpuct=4.0, x_noise=0.25, alpha=1.0, blocks_per_tree=0, device=None, search_threads=1):
         if not torch.cuda.is_available():
             raise _lib.SpmctsError("the HIP arena needs a GPU (torch.cuda.is_available() is False)")
         gid, W, H, A = GAMES[game]
@@ -69,6 +69,9 @@ class Arena:
         cfg.leaf_format = LEAF_FORMATS[leaf_format]
         cfg.leaf_layout = _lib.NHWC if leaf_layout == "nhwc" else _lib.NCHW
         cfg.compact = 1
+        # K simulations in flight per tree with virtual loss (mcts.py:328-331); rows = n_trees * K
+        self.search_threads = K = max(1, int(search_threads))
+        cfg.search_threads = K
         cfg.cpuct, cfg.x_noise, cfg.alpha = float(cpuct), float(x_noise), float(alpha)
         cfg.seed, cfg.subsequence0 = int(seed) & (2**64 - 1), int(subsequence0)
         self.cfg = cfg
@@ -81,7 +84,7 @@ class Arena:
         call("spmcts_arena_geometry", h, *[ctypes.byref(g) for g in geo])
         self.blocks_per_tree = geo[3].value
         dev = self.device
-        rows = max(n_trees, n_games, 1)
+        rows = max(n_trees * K, n_games, 1)
         self.max_rows = rows
         if leaf_format == "board":
             self._leaves = torch.zeros((rows, W, H), dtype=torch.int64, device=dev)
@@ -95,7 +98,7 @@ class Arena:
         self._i32 = torch.zeros(rows, dtype=torch.int32, device=dev)
         self._i8 = torch.zeros(rows, dtype=torch.int8, device=dev)
         self.n_active = 0
-        self.seg1 = n_trees  # first leaf row of network 1 (two-network arenas)
+        self.seg1 = n_trees * K  # first leaf row of network 1 (two-network arenas)
         self._L = L
 
     # ------------------------------------------------------------------ lifetime
@@ -273,9 +276,10 @@ class Arena:
 
     def leaf_trees(self, n):
         """Tree id of each of the first n leaf rows (device int32 tensor)."""
-        out = torch.empty(self.n_trees, dtype=torch.int32, device=self.device)
+        out = torch.empty(self.n_trees * self.search_threads, dtype=torch.int32, device=self.device)
         call("spmcts_leaf_trees", self.h, ptr(out), _stream())
-        return out[:n]
+        out = out[:n]
+        return out // self.search_threads if self.search_threads > 1 else out
 
     def root_stats(self, tree):
         A, cells = self.A, self.cells

@@ -75,6 +75,8 @@ typedef rocrand_state_philox4x32_10 Philox;
 
 struct View {
   int T, cap, G, A;
+  int iters;  // MCTreeSearch.iterations (bounds the last step of a K-in-flight search)
+  int K, NS;  // simulations in flight per tree (virtual loss; 1 = sequential), pending slots = T * K
   double cpuct, x, alpha;
   int strong, evaluate, rng_mode, leaf_format, leaf_layout;
   // node store
@@ -84,6 +86,7 @@ struct View {
   int32_t *bc;
   uint32_t *bvm;
   uint8_t *bf64;  // "w is a numpy float64" (strong_play dtype quirk, mcts.py:287/:308)
+  int32_t *bvl;   // MCNode.virtual_loss (mcts.py:44), allocated only when K > 1
   // trees
   int32_t *root;
   uint64_t *rpos, *rneg;
@@ -107,7 +110,8 @@ struct View {
   int64_t *tape_cur;        // [T]
   int64_t *cnt;             // per-tree counters [T][8]
   int32_t *active;
-  int32_t *row_tree;
+  int32_t *row_tree;  // row -> pending slot (tree * K + j)
+  int32_t *srow;      // pending slot -> row (K > 1)
   int32_t *row_count;
   float *root_prior;
   uint32_t *err;
@@ -141,7 +145,7 @@ struct View {
   int32_t sim;       // index of the current simulation within the search (by value per launch)
 };
 
-enum { C_SIMS = 0, C_NN = 1, C_TERM = 2, C_DEPTH = 3, C_SETNODE = 4, C_MOVES = 5, C_NCNT = 8 };
+enum { C_SIMS = 0, C_NN = 1, C_TERM = 2, C_DEPTH = 3, C_SETNODE = 4, C_MOVES = 5, C_LEAK = 6, C_NCNT = 8 };
 enum { GS_IDLE = 0, GS_ACTIVE = 1, GS_DONE = 2 };
 
 __device__ __forceinline__ void set_err(const View &v, uint32_t f) { atomicOr(v.err, f); }
@@ -239,6 +243,10 @@ __device__ __forceinline__ void reset_tree(const View &v, int tree, int player, 
   v.bp[nb + 0] = 0.f;
   v.bc[nb + 0] = 1;
   v.bf64[nb + 0] = 0;
+  if (v.K > 1) {
+    v.bvl[nb + 0] = 0;
+    for (int j = 0; j < P; ++j) v.bvl[nb + P + j] = 0;
+  }
   for (int j = 0; j < P; ++j) {
     v.bn[nb + P + j] = 0;
     v.bw[nb + P + j] = 0.0;
@@ -254,7 +262,7 @@ __device__ __forceinline__ void reset_tree(const View &v, int tree, int player, 
   v.rneg[tree] = 0;
   v.rplayer[tree] = (int8_t)player;
   v.noise_on[tree] = 0;
-  v.need[tree] = 0;
+  for (int j = 0; j < v.K; ++j) v.need[(size_t)tree * v.K + j] = 0;
 }
 
 // terminal value of _expand_node (mcts.py:305-313); r = reward * mover
@@ -481,6 +489,156 @@ __global__ __launch_bounds__(64) void k_select(View v, int n_active) {
 }
 
 // ----------------------------------------------------------------------------
+// kernel: select with K simulations in flight per tree (threaded search_node with virtual
+// loss, mcts.py:328-331 / :340-367).  The reference's threads interleave nondeterministically;
+// this kernel fixes the interleaving in which all K threads of a step select before any network
+// reply: sim j of the step walks the tree with the virtual loss of sims 0..j-1 in place (vl += 1
+// on every node it passes, mcts.py:345), sees their pending leaves as locked (score -1e10,
+// mcts.py:86-88, :347), and a terminal leaf is backed up at once with its path's vl removed.  A
+// node whose children are all invalid or locked ends the sim with its vl left in place
+// (mcts.py:349-354).  Pending leaves go to slot tree * K + j; k_expand_vl backs them up in j
+// order.  Locked = child-block index -2 while the leaf waits for the network.
+// ----------------------------------------------------------------------------
+template <class G>
+__global__ __launch_bounds__(64) void k_select_vl(View v, int n_active) {
+  constexpr int P = G::APAD;
+  constexpr int GPB = 64 / P;
+  __shared__ int32_t s_node[GPB][G::MAXD];
+
+  const int lane = threadIdx.x & (P - 1);
+  const int grp = threadIdx.x / P;
+  const int slot = blockIdx.x * GPB + grp;
+  if (slot >= n_active) return;
+  const int tree = v.active[slot];
+  if (tree < 0) return;
+
+  const size_t nb = nbase<G>(v, tree);
+  const size_t bb = (size_t)tree * v.cap;
+  const bool noise = v.noise_on[tree] != 0;
+  const double nz = (noise && lane < G::A) ? v.noise[(size_t)tree * P + lane] : 0.0;
+  const int gbase = (threadIdx.x & 63) & ~(P - 1);
+  TreeRng rng;
+  rng_load(v, tree, rng);
+  bool terr = false;
+  int64_t *cnt = v.cnt + (size_t)tree * C_NCNT;
+
+  const int limit = min(v.budget[tree], v.iters);
+  for (int j = 0; j < v.K; ++j) {
+    if (v.sim + j >= limit) break;
+    const int ps = tree * v.K + j;
+    int node = v.root[tree];
+    Board b{v.rpos[tree], v.rneg[tree]};
+    int player = v.rplayer[tree];
+    int node_n = v.bn[nb + node];
+    int node_vl = v.bvl[nb + node] + 1;  // this sim's virtual loss on the node (mcts.py:345)
+    int cb = v.bc[nb + node];
+    int depth = 0;
+    for (;;) {
+      if (lane == 0) {
+        s_node[grp][depth] = node;
+        v.bvl[nb + node] = node_vl;
+      }
+      if (cb < 0) {
+        if (lane == 0) set_err(v, SPMCTS_ERR_STATE);
+        return;
+      }
+      const uint32_t vm = v.bvm[bb + cb];
+      const size_t ci = nb + (size_t)cb * P + lane;
+      int cn = 0, cc = -1, cvl = 0;
+      double cw = 0.0;
+      float cp = 0.f;
+      if (lane < G::A) {
+        cn = v.bn[ci];
+        cw = v.bw[ci];
+        cp = v.bp[ci];
+        cc = v.bc[ci];
+        cvl = v.bvl[ci];
+      }
+      // valid (mcts.py:86-88): valid move and not locked by a pending sim
+      const bool valid = (lane < G::A) && ((vm >> lane) & 1u) && cc != -2;
+      double score = -10000000000.0;
+      if (valid) {
+        // q (mcts.py:59-62): (w - vl) / (n + vl)
+        const int ne = cn + cvl;
+        const double q = ne ? (cw - (double)cvl) / (double)ne : 0.0;
+        const double pe = (depth == 0 && noise) ? nz * v.x + (double)cp * (1.0 - v.x) : (double)cp;
+        // u (mcts.py:71-78): sqrt(parent.n + parent.virtual_loss) / (1 + n + virtual_loss)
+        const double u = ((v.cpuct * pe) * sqrt((double)(node_n + node_vl))) / (double)(1 + cn + cvl);
+        score = (player > 0 ? q : -q) + u;
+      }
+      if (!group_or<P>(valid ? 1 : 0)) {  // mcts.py:349-354: return, virtual loss left in place
+        if (lane == 0) cnt[C_LEAK] += 1;
+        break;
+      }
+      double s = -INFINITY;
+      if (lane < G::A) s = score + 0.000001 * rng_lane(v, rng, lane, &terr);
+      rng_advance(v, rng, G::A);
+      int a = lane;
+      group_argmax<P>(s, a);
+      const int cc_a = __shfl(cc, gbase + a, 64);
+      const int cn_a = __shfl(cn, gbase + a, 64);
+      const int cvl_a = __shfl(cvl, gbase + a, 64);
+      const int child = cb * P + a;
+      if (cc_a < 0) {
+        // leaf: _expand_node (mcts.py:301-321)
+        Board nb2 = b;
+        int rew = 0, done = 0;
+        const int st = step<G>(nb2, a, player, &rew, &done);
+        if (lane == 0) {
+          if (st != STEP_OK) set_err(v, SPMCTS_ERR_STATE);
+          cnt[C_SIMS] += 1;
+          cnt[C_DEPTH] += depth + 1;
+          if (done) {
+            // terminal: backup (mcts.py:94-98) then remove the path's virtual loss (:365)
+            const double val = terminal_value(v, b, rew * player);
+            v.bn[nb + child] += 1;
+            v.bw[nb + child] += val;
+            if (v.strong) v.bf64[nb + child] = 1;
+            for (int k = 0; k <= depth; ++k) {
+              const size_t idx = nb + s_node[grp][k];
+              v.bn[idx] += 1;
+              v.bw[idx] += val;
+              if (v.strong) v.bf64[idx] = 1;
+              v.bvl[idx] -= 1;
+            }
+            cnt[C_TERM] += 1;
+          } else {
+            // lock the leaf (mcts.py:359) and stash the path for k_expand_vl
+            v.bc[nb + child] = -2;
+            const size_t pb = (size_t)ps * G::MAXD;
+            for (int k = 0; k <= depth; ++k) v.pnode[pb + k] = s_node[grp][k];
+            v.plen[ps] = depth + 1;
+            v.leaf[ps] = child;
+            v.lpos[ps] = nb2.pos;
+            v.lneg[ps] = nb2.neg;
+            v.lmover[ps] = (int8_t)player;
+            v.need[ps] = 1;
+          }
+        }
+        break;
+      }
+      play<G>(b, a, player);
+      node = child;
+      node_n = cn_a;
+      node_vl = cvl_a + 1;
+      cb = cc_a;
+      player = -player;
+      ++depth;
+      if (depth >= G::MAXD) {
+        if (lane == 0) set_err(v, SPMCTS_ERR_STATE);
+        return;
+      }
+    }
+    // the next sim reads what this one wrote (lane 0's stores, other lanes' loads)
+    __threadfence();
+  }
+  if (lane == 0) {
+    if (terr) set_err(v, SPMCTS_ERR_TAPE);
+    rng_store(v, tree, rng);
+  }
+}
+
+// ----------------------------------------------------------------------------
 // kernel: compaction of pending leaves into rows (tree order => deterministic)
 // ----------------------------------------------------------------------------
 // Two segments: leaves of network-0 trees in rows [0, n0), of network-1 trees in rows
@@ -489,13 +647,13 @@ __global__ __launch_bounds__(64) void k_select(View v, int n_active) {
 __global__ __launch_bounds__(1024) void k_scan_need(View v, int32_t *count_out) {
   __shared__ int32_t s_p0[1024], s_p1[1024];
   const int tid = threadIdx.x;
-  const int T = v.T;
+  const int T = v.NS;  // pending slots (tree * K + j), tree order then in-flight order
   const int chunk = (T + 1023) / 1024;
   const int lo = min(T, tid * chunk), hi = min(T, lo + chunk);
   int c0 = 0, c1 = 0;
   for (int t = lo; t < hi; ++t)
     if (v.need[t]) {
-      if (v.tnet[t]) ++c1; else ++c0;
+      if (v.tnet[t / v.K]) ++c1; else ++c0;
     }
   s_p0[tid] = c0;
   s_p1[tid] = c1;
@@ -512,7 +670,9 @@ __global__ __launch_bounds__(1024) void k_scan_need(View v, int32_t *count_out) 
   int r0 = s_p0[tid] - c0, r1 = v.seg1 + s_p1[tid] - c1;
   for (int t = lo; t < hi; ++t)
     if (v.need[t]) {
-      if (v.tnet[t]) v.row_tree[r1++] = t; else v.row_tree[r0++] = t;
+      const int r = v.tnet[t / v.K] ? r1++ : r0++;
+      v.row_tree[r] = t;
+      if (v.K > 1) v.srow[t] = r;
     }
   if (tid == 1023) {
     v.row_count[0] = s_p0[1023];
@@ -537,7 +697,7 @@ __global__ void k_encode(View v, void *out) {
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int row = (int)(gid / G::CELLS);
   const int cell = (int)(gid % G::CELLS);
-  if (row >= v.T || !row_live(v, row)) return;
+  if (row >= v.NS || !row_live(v, row)) return;
   const int t = v.row_tree[row];
   const int x = cell / G::H, y = cell % G::H;
   const uint64_t bit = 1ull << cell_bit<G>(x, y);
@@ -630,6 +790,65 @@ __global__ __launch_bounds__(64) void k_expand(View v, const float *probs0, cons
 }
 
 // ----------------------------------------------------------------------------
+// kernel: expand + backup of the K pending leaves of each tree, in in-flight order j (the
+// replies of the threaded search, mcts.py:360-365): create_children, backup (n += 1, w += v on
+// the leaf and its path), unlock, vl -= 1 on the path.  Read-modify-write: earlier slots of the
+// same tree have changed the shared ancestors.
+// ----------------------------------------------------------------------------
+template <class G>
+__global__ __launch_bounds__(64) void k_expand_vl(View v, const float *probs0, const float *values0,
+                                                  const float *probs1, const float *values1) {
+  constexpr int P = G::APAD;
+  const int lane = threadIdx.x & (P - 1);
+  const int tree = (blockIdx.x * blockDim.x + threadIdx.x) / P;
+  if (tree >= v.T) return;
+  const size_t nb = nbase<G>(v, tree);
+  const size_t bb = (size_t)tree * v.cap;
+  for (int j = 0; j < v.K; ++j) {
+    const int ps = tree * v.K + j;
+    if (!v.need[ps]) continue;
+    const int row = v.srow[ps];
+    const bool s1 = row >= v.seg1;
+    const float *prow = s1 ? probs1 + (size_t)(row - v.seg1) * G::A : probs0 + (size_t)row * G::A;
+    const float vrow = s1 ? values1[row - v.seg1] : values0[row];
+    const int blk = v.used[tree];
+    if (blk >= v.cap) {
+      if (lane == 0) set_err(v, SPMCTS_ERR_POOL);
+      return;
+    }
+    const int leaf = v.leaf[ps];
+    {
+      const size_t ci = nb + (size_t)blk * P + lane;
+      v.bn[ci] = 0;
+      v.bw[ci] = 0.0;
+      v.bp[ci] = lane < G::A ? prow[lane] : 0.f;
+      v.bc[ci] = -1;
+      v.bf64[ci] = 0;
+      v.bvl[ci] = 0;
+    }
+    if (lane == 0) {
+      const double val = (double)vrow * (double)v.lmover[ps];
+      v.bvm[bb + blk] = legal_mask<G>(Board{v.lpos[ps], v.lneg[ps]});
+      v.bc[nb + leaf] = blk;
+      v.bn[nb + leaf] += 1;
+      v.bw[nb + leaf] += val;
+      const int plen = v.plen[ps];
+      const size_t pb = (size_t)ps * G::MAXD;
+      for (int k = 0; k < plen; ++k) {
+        const size_t idx = nb + v.pnode[pb + k];
+        v.bn[idx] += 1;
+        v.bw[idx] += val;
+        v.bvl[idx] -= 1;
+      }
+      v.used[tree] = blk + 1;
+      v.need[ps] = 0;
+      v.cnt[(size_t)tree * C_NCNT + C_NN] += 1;
+    }
+    __threadfence();
+  }
+}
+
+// ----------------------------------------------------------------------------
 // _play (mcts.py:272-299): choose the move from root visit counts
 // ----------------------------------------------------------------------------
 struct PlayOut {
@@ -698,7 +917,13 @@ __device__ PlayOut play_move_choice(const View &v, int tree, double temp, float 
     o.recorded = true;
     for (int j = 0; j < G::A; ++j) probs_out[j] = (float)pr[j];
     const int rn = v.bn[nb + root];
-    o.q = rn ? v.bw[nb + root] / (double)rn : 0.0;
+    if (v.K > 1) {
+      // q (mcts.py:59-62) with the root's virtual loss, nonzero after a leaked sim (:349-354)
+      const int rvl = v.bvl[nb + root];
+      o.q = (rn + rvl) ? (v.bw[nb + root] - (double)rvl) / (double)(rn + rvl) : 0.0;
+    } else {
+      o.q = rn ? v.bw[nb + root] / (double)rn : 0.0;
+    }
     o.qf64 = v.bf64[nb + root];
   } else {
     int best = 0;
@@ -760,14 +985,15 @@ __device__ bool set_node(const View &v, int tree, int a) {
       v.bw[nb + child] = v.bw[nb + child] + val;
       if (v.strong) v.bf64[nb + child] = 1;
     } else {
-      v.plen[tree] = 0;
-      v.leaf[tree] = child;
-      v.leaf_n[tree] = 0;
-      v.leaf_w[tree] = v.bw[nb + child];
-      v.lpos[tree] = b.pos;
-      v.lneg[tree] = b.neg;
-      v.lmover[tree] = (int8_t)rp;
-      v.need[tree] = 1;
+      const int ps = tree * v.K;  // pending slot 0 of the tree
+      v.plen[ps] = 0;
+      v.leaf[ps] = child;
+      v.leaf_n[ps] = 0;
+      v.leaf_w[ps] = v.bw[nb + child];
+      v.lpos[ps] = b.pos;
+      v.lneg[ps] = b.neg;
+      v.lmover[ps] = (int8_t)rp;
+      v.need[ps] = 1;
     }
   }
   v.root[tree] = child;
@@ -1178,6 +1404,7 @@ static void plan_arena(spmcts_arena *h, Plan &pl) {
   pl.add(&v.bp, nodes);
   pl.add(&v.bc, nodes);
   pl.add(&v.bf64, nodes);
+  pl.add(&v.bvl, v.K > 1 ? nodes : 1);
   pl.add(&v.bvm, T * cap);
   pl.add(&v.root, T);
   pl.add(&v.rpos, T);
@@ -1186,23 +1413,25 @@ static void plan_arena(spmcts_arena *h, Plan &pl) {
   pl.add(&v.used, T);
   pl.add(&v.noise, T * P);
   pl.add(&v.noise_on, T);
-  pl.add(&v.pnode, T * h->maxd);
-  pl.add(&v.pn, T * h->maxd);
-  pl.add(&v.pw, T * h->maxd);
-  pl.add(&v.plen, T);
-  pl.add(&v.leaf, T);
-  pl.add(&v.leaf_n, T);
-  pl.add(&v.leaf_w, T);
-  pl.add(&v.lpos, T);
-  pl.add(&v.lneg, T);
-  pl.add(&v.lmover, T);
-  pl.add(&v.need, T);
+  const size_t NS = v.NS;  // pending slots
+  pl.add(&v.pnode, NS * h->maxd);
+  pl.add(&v.pn, NS * h->maxd);
+  pl.add(&v.pw, NS * h->maxd);
+  pl.add(&v.plen, NS);
+  pl.add(&v.leaf, NS);
+  pl.add(&v.leaf_n, NS);
+  pl.add(&v.leaf_w, NS);
+  pl.add(&v.lpos, NS);
+  pl.add(&v.lneg, NS);
+  pl.add(&v.lmover, NS);
+  pl.add(&v.need, NS);
   pl.add(&v.rng, T);
   pl.add((int64_t **)&v.tape_end, T);
   pl.add(&v.tape_cur, T);
   pl.add(&v.cnt, T * C_NCNT);
   pl.add(&v.active, std::max(T, G));
-  pl.add(&v.row_tree, T);
+  pl.add(&v.row_tree, NS);
+  pl.add(&v.srow, NS);
   pl.add(&v.row_count, 4);
   pl.add(&v.root_prior, 32);  // [net][16]
   pl.add(&v.err, 4);
@@ -1259,12 +1488,16 @@ static int setup_view(spmcts_arena *h, const spmcts_config *cfg) {
   v.rng_mode = cfg->rng_mode;
   v.leaf_format = cfg->leaf_format;
   v.leaf_layout = cfg->leaf_layout;
-  v.seg1 = v.T;
+  v.K = std::max(1, cfg->search_threads);
+  v.iters = std::max(1, cfg->iterations);
+  v.NS = v.T * v.K;
+  v.seg1 = v.NS;
   v.record = 1;
   v.sim = 0;
   if (v.T <= 0) return fail(-3, "n_trees must be > 0");
   if (v.G < 0 || 2 * (long long)v.G > v.T) return fail(-3, "games mode needs n_trees >= 2 * n_games");
   if (v.T > (1 << 24)) return fail(-3, "too many trees");
+  if (v.K > 64 || (long long)v.T * v.K > (1 << 24)) return fail(-3, "search_threads too large");
   if (v.cap < 4) return fail(-3, "blocks_per_tree too small");
   if ((long long)v.cap * P >= (1ll << 31)) return fail(-3, "blocks_per_tree too large");
   return 0;
@@ -1278,7 +1511,7 @@ __global__ void k_rng_init(View v, uint64_t seed, uint64_t sub0) {
   v.rng[t] = s;
   v.tape_cur[t] = 0;
   ((int64_t *)v.tape_end)[t] = 0;
-  v.need[t] = 0;
+  for (int j = 0; j < v.K; ++j) v.need[(size_t)t * v.K + j] = 0;
   v.noise_on[t] = 0;
   v.tnet[t] = 0;
   v.tkind[t] = SPMCTS_PLAYER_MCTS;
@@ -1455,7 +1688,7 @@ int spmcts_search_begin(spmcts_arena *h, const int32_t *trees_dev, int32_t n, sp
 static int launch_rows(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_dev, hipStream_t s) {
   hipLaunchKernelGGL(k_scan_need, dim3(1), dim3(1024), 0, s, h->v, leaf_count_dev);
   if (leaves_dev) {
-    const long long total = (long long)h->v.T * h->cells;
+    const long long total = (long long)h->v.NS * h->cells;
     DISPATCH(h, hipLaunchKernelGGL(k_encode<GG>, dim3(nblk(total, 256)), dim3(256), 0, s, h->v, leaves_dev));
   }
   LAUNCH_CHECK();
@@ -1468,9 +1701,13 @@ int spmcts_select_tree(spmcts_arena *h, spmcts_stream stream) {
   const int n = h->n_active;
   if (n > 0) {
     const int gpb = 64 / h->P;
-    DISPATCH(h, hipLaunchKernelGGL(k_select<GG>, dim3(nblk(n, gpb)), dim3(64), 0, s, h->v, n));
+    if (h->v.K > 1) {
+      DISPATCH(h, hipLaunchKernelGGL(k_select_vl<GG>, dim3(nblk(n, gpb)), dim3(64), 0, s, h->v, n));
+    } else {
+      DISPATCH(h, hipLaunchKernelGGL(k_select<GG>, dim3(nblk(n, gpb)), dim3(64), 0, s, h->v, n));
+    }
   }
-  h->v.sim += 1;
+  h->v.sim += h->v.K;
   LAUNCH_CHECK();
   return 0;
 }
@@ -1489,10 +1726,16 @@ int spmcts_select(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_dev, sp
 int spmcts_expand2(spmcts_arena *h, const float *probs0_dev, const float *values0_dev, const float *probs1_dev,
                    const float *values1_dev, spmcts_stream stream) {
   if (!h) return fail(-1, "null arena");
-  if (h->v.seg1 < h->v.T && (!probs1_dev || !values1_dev)) return fail(-1, "two-network arena needs network-1 outputs");
+  if (h->v.seg1 < h->v.NS && (!probs1_dev || !values1_dev))
+    return fail(-1, "two-network arena needs network-1 outputs");
   const int gpb = 64 / h->P;
-  DISPATCH(h, hipLaunchKernelGGL(k_expand<GG>, dim3(nblk(h->v.T, gpb)), dim3(64), 0, (hipStream_t)stream, h->v,
-                                 probs0_dev, values0_dev, probs1_dev, values1_dev));
+  if (h->v.K > 1) {
+    DISPATCH(h, hipLaunchKernelGGL(k_expand_vl<GG>, dim3(nblk(h->v.T, gpb)), dim3(64), 0, (hipStream_t)stream, h->v,
+                                   probs0_dev, values0_dev, probs1_dev, values1_dev));
+  } else {
+    DISPATCH(h, hipLaunchKernelGGL(k_expand<GG>, dim3(nblk(h->v.T, gpb)), dim3(64), 0, (hipStream_t)stream, h->v,
+                                   probs0_dev, values0_dev, probs1_dev, values1_dev));
+  }
   LAUNCH_CHECK();
   return 0;
 }
@@ -1501,7 +1744,7 @@ int spmcts_expand(spmcts_arena *h, const float *probs_dev, const float *values_d
   if (!h) return fail(-1, "null arena");
   // one buffer indexed by row: network-1 rows (if any) sit at their own row index
   const size_t s1 = (size_t)h->v.seg1;
-  const bool dual = h->v.seg1 < h->v.T;
+  const bool dual = h->v.seg1 < h->v.NS;
   return spmcts_expand2(h, probs_dev, values_dev, dual ? probs_dev + s1 * h->A : nullptr,
                         dual ? values_dev + s1 : nullptr, stream);
 }
@@ -1525,7 +1768,7 @@ int spmcts_set_tree_players(spmcts_arena *h, const uint8_t *nets, const uint8_t 
   HIP_TRY(hipMemcpy(h->v.tnet, nt.data(), T, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(h->v.tkind, kd.data(), T, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(h->v.budget, bd.data(), 4 * (size_t)T, hipMemcpyHostToDevice));
-  h->v.seg1 = n0;  // network-0 trees never have more than n0 pending leaves
+  h->v.seg1 = n0 * h->v.K;  // network-0 trees never have more than n0 * K pending leaves
   return 0;
 }
 
@@ -1573,7 +1816,7 @@ int spmcts_play_action(spmcts_arena *h, const int32_t *trees_dev, const int32_t 
 
 int spmcts_leaf_trees(spmcts_arena *h, int32_t *trees_dev, spmcts_stream stream) {
   if (!h || !trees_dev) return fail(-1, "null argument");
-  HIP_TRY(hipMemcpyAsync(trees_dev, h->v.row_tree, sizeof(int32_t) * h->v.T, hipMemcpyDeviceToDevice,
+  HIP_TRY(hipMemcpyAsync(trees_dev, h->v.row_tree, sizeof(int32_t) * h->v.NS, hipMemcpyDeviceToDevice,
                          (hipStream_t)stream));
   return 0;
 }

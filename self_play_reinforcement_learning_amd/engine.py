@@ -86,7 +86,7 @@ class SelfPlayEngine:
     def __init__(self, game, network, n_games=4096, iterations=200, alpha=1.0, strong_play=False, evaluate=False,
                  seed=0, subsequence0=None, rng="philox", max_games=None, device=None, dtype=torch.bfloat16,
                  leaf_layout="nhwc", cpuct=4.0, x_noise=0.25, blocks_per_tree=0, bucket=256, opponent=None,
-                 opponent_iterations=None, record=True):
+                 opponent_iterations=None, record=True, search_threads=1):
         self.game = game
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.evaluator = make_evaluator(network, game, device=self.device, dtype=dtype, leaf_layout=leaf_layout)
@@ -114,7 +114,10 @@ class SelfPlayEngine:
                            seed=seed, subsequence0=subsequence0, strong_play=strong_play, evaluate=evaluate,
                            leaf_format=self.evaluator.leaf_format, leaf_layout=self.evaluator.leaf_layout,
                            cpuct=cpuct, x_noise=x_noise, alpha=alpha, blocks_per_tree=blocks_per_tree,
-                           device=self.device)
+                           device=self.device, search_threads=search_threads)
+        # K sims in flight per tree (the reference's thread_count search, mcts.py:328-331)
+        self.search_threads = self.arena.search_threads
+        self.select_steps = -(-self.iterations // self.search_threads)
         if self.evaluator1 is not None or opp_kind != _lib.PLAYER_MCTS or it1 != iterations:
             # tree 2g = the policy, 2g + 1 = the opposing player (selfplayworker.py:164-176)
             self.arena.set_tree_players(nets=[0, 1 if self.evaluator1 is not None else 0] * n_games,
@@ -243,11 +246,11 @@ class SelfPlayEngine:
     def _ply_simulation(self):
         """One lock-step simulation of every searching tree, without a host synchronisation."""
         self.arena.select_async(self.select_timer)
-        self._eval_expand_dev(cap=self.n_games)
+        self._eval_expand_dev(cap=self.n_games * self.search_threads)
 
     def _ply_move(self):
         self.arena.games_end_ply_async()
-        self._eval_expand_dev()
+        self._eval_expand_dev(cap=2 * self.n_games)
 
     def ply(self, on_moves=None, refill=True, game_offset=0):
         """Advance every active game by one move. Returns (#games finished, #records exported).
@@ -255,11 +258,11 @@ class SelfPlayEngine:
         self._ply_begin()
         a = self.arena
         if self._device_count_ok():
-            for _ in range(self.iterations):
+            for _ in range(self.select_steps):
                 self._ply_simulation()
             self._ply_move()
         else:
-            for _ in range(self.iterations):
+            for _ in range(self.select_steps):
                 self._eval_expand(a.select(self.select_timer))
             self._eval_expand(a.games_end_ply())
         return self._ply_finish(on_moves, refill, game_offset)
@@ -410,6 +413,7 @@ class LanedEngine:
                         ev.concurrent = True
         self.n_games = n_games
         self.iterations = self.lanes[0].iterations
+        self.select_steps = self.lanes[0].select_steps
         self.evaluator = self.lanes[0].evaluator
         self.select_timer = self.nn_timer = self.tower_timer = None
 
@@ -466,7 +470,7 @@ class LanedEngine:
                     res.append(e.ply(on_moves, refill, game_offset=i * self.GAME_ID_STRIDE))
         else:
             self._each(lambda e: e._ply_begin())
-            for _ in range(self.iterations):
+            for _ in range(self.select_steps):
                 self._each(lambda e: e._ply_simulation())
             self._each(lambda e: e._ply_move())
             res = []

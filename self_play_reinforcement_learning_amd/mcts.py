@@ -60,7 +60,7 @@ class MCTreeSearch(Policy):
     def __init__(self, network=None, env=None, optim=None, memory_queue=None, iterations=100, temperature_cutoff=5,
                  batch_size=64, memory_size=200000, min_memory=20000, update_nn=True, starting_state_dict=None,
                  thread_count=4, strong_play=False, q_average=True, alpha=1, env_gen=None, evaluator=None,
-                 seed=None, device=None, rng="philox", cpuct=4, x_noise=0.25):
+                 seed=None, device=None, rng="philox", cpuct=4, x_noise=0.25, threading=False):
         network = network if network is not None else evaluator
         env = env if env is not None else env_gen
         if network is None or env is None:
@@ -85,14 +85,17 @@ class MCTreeSearch(Policy):
         self.starting_state_dict = starting_state_dict
         self.thread_count = thread_count
         self.evaluating = False
-        self.threading = False  # one simulation in flight per tree (the reference's sequential mode)
+        # threading=True: thread_count sims in flight with virtual loss, the reference's mode when its
+        # network is an InferenceProxy (mcts.py:154, :328-331); False: its sequential mode
+        self.threading = bool(threading)
+        k = int(thread_count) if self.threading and thread_count and thread_count > 1 else 1
         self._evaluator = make_evaluator(network, self.game, device=self.device)
         if seed is None:
             seed = int(np.random.randint(0, 2**31 - 1))
         self._arena = Arena(self.game, n_trees=1, n_games=0, iterations=iterations, rng=rng, seed=seed,
                             strong_play=strong_play, leaf_format=self._evaluator.leaf_format,
                             leaf_layout=self._evaluator.leaf_layout, cpuct=cpuct, x_noise=x_noise, alpha=alpha,
-                            device=self.device)
+                            device=self.device, search_threads=k)
         self.temp_memory = []
         self.moves_played = 0
         self._root_prior_stale = True
@@ -133,7 +136,7 @@ class MCTreeSearch(Policy):
     def search(self):
         a = self._arena
         a.search_begin([0])
-        for _ in range(self.iterations):
+        for _ in range(-(-self.iterations // a.search_threads)):
             self._eval_expand(a.select())
 
     def _play(self, temp=1):

@@ -118,6 +118,7 @@ class _FakeLane(_FakeEngine):
     """A LanedEngine lane: the phase methods of SelfPlayEngine.ply; finishes `rate` games per ply."""
 
     iterations = 3
+    select_steps = 3
 
     def _device_count_ok(self):
         return True
@@ -150,6 +151,7 @@ def _laned_worker(rank, world, port, q):
     eng.lanes = [_FakeLane(rate=rank + 1), _FakeLane(rate=1)]
     eng.streams = [None, None]
     eng.iterations = 3
+    eng.select_steps = 3
     eng.device = torch.device("cpu")
     games = []
 

@@ -202,3 +202,36 @@ def test_sqrt_and_division_are_ieee():
     for c, r in zip(cases, res):
         assert r["child_w"] == c["child_w"]
     assert Arena is not None
+
+
+# ----------------------------------------------------------------- threaded (virtual-loss) mode
+def _threaded_groups():
+    cases = [c for c in load_json("mcts_search.json")]
+    return sorted(group_by(cases, ("game", "sims", "strong_play")).items())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads", [2, 4, 8])
+@pytest.mark.parametrize("key", [k for k, _ in _threaded_groups()])
+def test_threaded_search_matches_oracle(key, threads):
+    """k_select_vl / k_expand_vl vs the oracle's threaded restatement (mcts.py:328-367, one fixed
+    interleaving), bit-exact on the same RNG tapes."""
+    from tests.parity_helpers import g2_threaded
+
+    cases = dict(_threaded_groups())[key]
+    runs = [g2_threaded(c, threads) for c in cases]
+    res, counters = run_g2_group(cases, search_threads=threads, tapes=[t for t, _ in runs])
+    assert counters["error_flags"] == 0
+    assert counters["sims"] == sum(e["stats"]["sims"] for _, e in runs)
+    assert counters["terminal_leaves"] == sum(e["stats"]["terminal_leaves"] for _, e in runs)
+    for c, (_, e), r in zip(cases, runs, res):
+        assert r["child_n"] == e["child_n"], c["id"]
+        assert r["child_w"] == e["child_w"], c["id"]
+        assert r["root_n"] == e["root_n"] and r["root_w"] == e["root_w"], c["id"]
+        assert r["action"] == e["action"], c["id"]
+        assert r["recorded"] == e["recorded"], c["id"]
+        if e["recorded"]:
+            assert r["state"] == e["state"], c["id"]
+            assert r["tree_probs"] == e["tree_probs"], c["id"]
+            q = np.float64(r["q"]) if r["q_f64"] else np.float32(r["q"])
+            assert float(q) == e["q"], c["id"]

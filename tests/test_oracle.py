@@ -163,3 +163,63 @@ def test_evaluation_games_match_reference(idx):
         lg = Log(g["seed"])
         _g5_run(g, rng_o=lg)
         assert lg.log == g["choices"]
+
+
+# ----------------------------------------------------------------- threaded (virtual-loss) mode
+def _threaded_tree(c, threads):
+    net = TableNet(A_OF[c["game"]], c["salt"])
+    np.random.seed(c["seed"])
+    t = OracleTree(c["game"], net, NumpyRNG(), c["sims"], strong_play=c["strong_play"], threads=threads)
+    for a in c["opening"]:
+        t.play_action(a)
+    return t
+
+
+def _walk(node):
+    yield node
+    for ch in node.children:
+        yield from _walk(ch)
+
+
+@pytest.mark.parametrize("idx", range(0, 182, 7))
+@pytest.mark.parametrize("threads", [2, 4, 8])
+def test_threaded_search_invariants(idx, threads):
+    """K sims in flight (mcts.py:328-331): every sim is backed up or leaks its path's virtual loss;
+    no lock survives the search; visit counts add up."""
+    c = load_json("mcts_search.json")[idx]
+    t = _threaded_tree(c, threads)
+    n0, s0 = t.root.n, dict(t.stats)
+    k0 = sum(ch.n for ch in t.root.children)
+    t.move()
+    sims = t.stats["sims"] - s0["sims"]
+    leaks = t.stats["leaks"] - s0["leaks"]
+    assert sims + leaks == c["sims"]
+    assert t.root.n - n0 == sims
+    nodes = list(_walk(t.root))
+    assert not any(x.locked for x in nodes)
+    assert all(x.vl >= 0 for x in nodes)
+    if leaks == 0:
+        assert all(x.vl == 0 for x in nodes)
+    else:
+        assert t.root.vl == leaks
+    assert sum(ch.n for ch in t.root.children) - k0 == sims  # each backed-up sim passes one root child
+
+
+def test_threaded_k1_is_the_sequential_search():
+    """threads=1 is the reference's sequential mode, pinned by the G2 fixtures."""
+    for c in load_json("mcts_search.json")[:40:3]:
+        a = _threaded_tree(c, 1)
+        act = a.move()
+        assert act == c["action"] and a.root_stats()["child_n"] == c["child_n"]
+
+
+def test_threaded_mode_changes_the_search():
+    """K > 1 spreads the in-flight sims over more children (virtual loss discourages re-selection)."""
+    cases = [c for c in load_json("mcts_search.json") if c["game"] == "connect4" and c["sims"] >= 25][:10]
+    differ = 0
+    for c in cases:
+        a, b = _threaded_tree(c, 1), _threaded_tree(c, 8)
+        a.move()
+        b.move()
+        differ += a.root_stats()["child_n"] != b.root_stats()["child_n"]
+    assert differ > 0
