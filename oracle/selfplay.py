@@ -14,7 +14,7 @@ from .mcts import OracleTree
 
 def play_episode(game, net_policy, net_opponent, rng_policy, rng_opponent, iterations, swap_sides=False,
                  update=True, evaluate=False, alpha=1, strong_play=False, on_ply=None, opponent="mcts",
-                 opponent_iterations=None):
+                 opponent_iterations=None, threads=1):
     """SelfPlayer.play_episode (selfplayworker.py:172-194).
 
     The reference draws every random number from ONE global RandomState, in
@@ -27,15 +27,17 @@ def play_episode(game, net_policy, net_opponent, rng_policy, rng_opponent, itera
 
     Returns (result r in the policy's frame, moves pushed to the memory queue in
     push order [policy's then opponent's], per-ply log).
+
+    threads=K > 1: both trees search with K sims in flight (oracle/mcts.py threaded mode).
     """
     env = make_env(game)
     env.reset()
     pol = OracleTree(game, net_policy, rng_policy, iterations, alpha, strong_play, evaluate=evaluate,
-                     root_player=(-1 if swap_sides else 1))
+                     root_player=(-1 if swap_sides else 1), threads=threads)
     if opponent == "mcts":
         opp = OracleTree(game, net_opponent, rng_opponent,
                          iterations if opponent_iterations is None else opponent_iterations, alpha, strong_play,
-                         evaluate=evaluate, root_player=(1 if swap_sides else -1))
+                         evaluate=evaluate, root_player=(1 if swap_sides else -1), threads=threads)
     else:
         opp = HardcodedPlayer(opponent, game, rng_opponent)
         opp.reset(1 if swap_sides else -1)

@@ -235,3 +235,35 @@ def test_threaded_search_matches_oracle(key, threads):
             assert r["tree_probs"] == e["tree_probs"], c["id"]
             q = np.float64(r["q"]) if r["q_f64"] else np.float32(r["q"])
             assert float(q) == e["q"], c["id"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads", [3, 4])
+@pytest.mark.parametrize("key", [k for k, _ in _g3_groups()])
+def test_threaded_selfplay_games_match_oracle(key, threads):
+    """Whole self-play games in games mode with K sims in flight per tree (set_node expansions in
+    slot 0 of the tree, budget-bounded last step), bit-exact vs the oracle's threaded episodes."""
+    from tests.parity_helpers import g3_tapes
+
+    games = dict(_g3_groups())[key]
+    moves, counters = run_g3_group(games, search_threads=threads)
+    assert counters["error_flags"] == 0
+    assert counters["games_finished"] == len(games)
+    exp_results = np.zeros((2, 3), dtype=np.int64)
+    by_game = {}
+    for i in range(len(moves["z"])):
+        by_game.setdefault(int(moves["game"][i]), []).append(i)
+    for gi, g in enumerate(games):
+        _, _, (r, exp_moves, _) = g3_tapes(g, threads)
+        exp_results[int(g["swap_sides"])][{1: 0, 0: 1, -1: 2}[r]] += 1
+        if g["evaluate"]:
+            continue
+        rows = by_game.get(gi, [])
+        assert len(rows) == len(exp_moves), gi
+        for i, M in zip(rows, exp_moves):
+            assert moves["state"][i].astype(int).tolist() == M["state"].reshape(-1).astype(int).tolist(), (gi, i)
+            assert float(moves["z"][i]) == float(M["actual_val"]), (gi, i)
+            assert moves["tree_probs"][i].astype(float).tolist() == M["tree_probs"].astype(float).tolist(), (gi, i)
+            q = np.float64(moves["q"][i]) if moves["q_f64"][i] else np.float32(moves["q"][i])
+            assert float(q) == float(M["q"]), (gi, i)
+    assert np.array_equal(np.array(counters["results"]), exp_results)

@@ -223,3 +223,22 @@ def test_threaded_mode_changes_the_search():
         b.move()
         differ += a.root_stats()["child_n"] != b.root_stats()["child_n"]
     assert differ > 0
+
+
+@pytest.mark.parametrize("idx", range(0, 12, 3))
+def test_threaded_episode_completes(idx):
+    """oracle play_episode with K=4 sims in flight: a finished game, one Move per searched ply."""
+    from oracle.selfplay import play_episode
+    from oracle.mcts import RecordingRNG
+
+    g = load_json("selfplay_games.json")[idx]
+    A = A_OF[g["game"]]
+    np.random.seed(g["seed"])
+    base = NumpyRNG()
+    r, moves, log, (pol, opp, env) = play_episode(g["game"], TableNet(A, g["salt_policy"]), TableNet(A, g["salt_policy"]),
+                                                  RecordingRNG(base), RecordingRNG(base), g["sims"],
+                                                  swap_sides=g["swap_sides"], threads=4)
+    assert r in (-1, 0, 1)
+    assert len(moves) == sum(1 for e in log if e["q"] is not None)
+    for t in (pol, opp):
+        assert all(x.vl >= 0 and not x.locked for x in _walk(t.root))
