@@ -137,9 +137,10 @@ def main():
                     help="arenas per GPU on their own HIP streams (engine.LanedEngine); 1 = one arena")
     ap.add_argument("--no-pack", action="store_true",
                     help="lanes > 1: keep round-aligned tower tiles (no SPMCTS_TOWER_PACK)")
-    ap.add_argument("--search-threads", type=int, default=1,
-                    help="sims in flight per tree with virtual loss (the reference's thread_count search, "
-                         "mcts.py:328-331); 1 = sequential search (bit-exact to the reference's sequential mode)")
+    ap.add_argument("--search-threads", type=int, default=4,
+                    help="sims in flight per tree with virtual loss: the reference's thread_count search "
+                         "(mcts.py:328-331), 4 in its headline self-play setup (InferenceProxy workers, "
+                         "SURVEY §6); 1 = sequential search (bit-exact to the reference's sequential fixtures)")
     args = ap.parse_args()
     arena_mode = args.mode == "arena"
 

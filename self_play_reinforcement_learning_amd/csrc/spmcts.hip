@@ -629,8 +629,9 @@ __global__ __launch_bounds__(64) void k_select_vl(View v, int n_active) {
         return;
       }
     }
-    // the next sim reads what this one wrote (lane 0's stores, other lanes' loads)
-    __threadfence();
+    // the next sim reads what this one wrote (lane 0's stores, other lanes' loads): one wave owns
+    // the tree, so a workgroup-scope fence (stores complete, same CU's L1) is enough
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   }
   if (lane == 0) {
     if (terr) set_err(v, SPMCTS_ERR_TAPE);
@@ -844,7 +845,7 @@ __global__ __launch_bounds__(64) void k_expand_vl(View v, const float *probs0, c
       v.need[ps] = 0;
       v.cnt[(size_t)tree * C_NCNT + C_NN] += 1;
     }
-    __threadfence();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   }
 }
 

@@ -414,6 +414,7 @@ class LanedEngine:
         self.n_games = n_games
         self.iterations = self.lanes[0].iterations
         self.select_steps = self.lanes[0].select_steps
+        self.search_threads = self.lanes[0].search_threads
         self.evaluator = self.lanes[0].evaluator
         self.select_timer = self.nn_timer = self.tower_timer = None
 

@@ -142,8 +142,12 @@ class SelfPlayScheduler:
         n_games = self.n_games or max(64, min(4096, (num_workers or 1) * threads_per_worker * 64))
         if resume_model:
             self._load_latest(prev_run=True)
+        # the reference's workers search with thread_count threads + virtual loss exactly when they
+        # talk to an InferenceProxy (mcts.py:154, self_play_parallel.py:95-171): K sims in flight
+        threads = int(kw.get("thread_count", 4) or 1) if inference_proxy else 1
         ekw = dict(iterations=kw.get("iterations", 100), alpha=kw.get("alpha", 1),
-                   strong_play=kw.get("strong_play", False), seed=self.seed + 7919 * self.rank, device=self.device)
+                   strong_play=kw.get("strong_play", False), seed=self.seed + 7919 * self.rank, device=self.device,
+                   search_threads=max(1, threads))
         lanes = self.lanes if self.lanes is not None else (2 if n_games >= 1024 else 1)
         if lanes > 1 and n_games >= 2 * lanes:
             self.engine = LanedEngine(self.game, self.network, n_games=n_games, lanes=lanes, **ekw)

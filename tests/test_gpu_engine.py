@@ -22,14 +22,17 @@ def _legal(game, board):
 
 @pytest.mark.parametrize("game,n_games,sims,ff,blocks", [("connect4", 64, 16, 4, 1), ("tictactoe", 64, 25, 4, 1),
                                                          ("connect4", 512, 8, 8, 2)])
-def test_engine_selfplay_invariants(game, n_games, sims, ff, blocks):
+@pytest.mark.parametrize("threads", [1, 4])
+def test_engine_selfplay_invariants(game, n_games, sims, ff, blocks, threads):
     from self_play_reinforcement_learning_amd.engine import SelfPlayEngine
     from self_play_reinforcement_learning_amd.modules import ResidualTower
 
     torch.manual_seed(0)
     W, H, A = (7, 6, 7) if game == "connect4" else (3, 3, 9)
     net = ResidualTower(W, H, A, num_blocks=blocks, filter_factor=ff)
-    eng = SelfPlayEngine(game, net, n_games=n_games, iterations=sims, seed=1, max_games=2 * n_games)
+    eng = SelfPlayEngine(game, net, n_games=n_games, iterations=sims, seed=1, max_games=2 * n_games,
+                         search_threads=threads)  # threads > 1: virtual-loss search (mcts.py:328-331)
+    assert eng.select_steps == -(-sims // threads)
     got = []
     eng.run(games=2 * n_games, on_moves=lambda m: got.append({k: v.cpu().numpy() for k, v in m.items()}))
     eng.check()
@@ -133,6 +136,7 @@ def test_scheduler_train_model_dropin(tmp_path, lanes):
                            n_games=16, lanes=lanes)
     sp.train_model(2)
     assert len(getattr(sp.engine, "lanes", [sp.engine])) == lanes
+    assert sp.engine.search_threads == 4  # inference_proxy=True: thread_count (default 4) sims in flight
     saves = sorted(p for p in (tmp_path / sp.start_time).iterdir() if p.name.startswith("model-"))
     assert len(saves) == 2
     ck = torch.load(saves[-1], weights_only=True)
@@ -354,3 +358,4 @@ def test_full_size_selfplay_properties():
     for gid in np.unique(moves["game"]):
         zs = moves["z"][moves["game"] == gid]
         assert (zs == 0).all() or sorted(np.unique(zs).tolist()) == [-1.0, 1.0]
+
