@@ -55,16 +55,18 @@ def head_linear_flops(W, H, A, filter_factor):
     return 2 * ff * cells * A + 2 * ff * cells * 8 * ff + 2 * 8 * ff
 
 
-def select_bytes(sims, levels, A=7):
+def select_bytes(sims, levels, A=7, threads=1):
     """Algorithmic HBM bytes moved by k_select.
 
     Per scored level: the child block (A x {n i32, w f64, p f32, child i32}) + vmask = 20A + 4
     (the next level's child-block index comes with the block).  Per simulation: tree header
     (active id, root id/board/player, noise flag, A noise doubles, root n/w/child index) +
     Philox state load/store = 90 + 8A + 128, leaf record writes (16 per path entry + 38).
+    k_select_vl (threads > 1) also reads the children's virtual loss (4A) and writes the node's
+    (4) per level, and the leaf's lock (4) per sim; its path record is 4 per entry, not 16.
     """
-    per_level = 20 * A + 4 + 16
-    per_sim = 90 + 8 * A + 128 + 38
+    per_level = 20 * A + 4 + 16 if threads <= 1 else 24 * A + 4 + 4 + 4
+    per_sim = 90 + 8 * A + 128 + 38 + (4 if threads > 1 else 0)
     return levels * per_level + sims * per_sim
 
 
@@ -216,7 +218,7 @@ def main():
     sel_launches = eng.select_timer.count()
     sims_local = c1["sims"] - c0["sims"]
     levels_local = c1["depth_sum"] - c0["depth_sum"]
-    sel_bytes = select_bytes(sims_local, levels_local)
+    sel_bytes = select_bytes(sims_local, levels_local, threads=args.search_threads)
     sel_avg_s = sel_ms / 1e3 / max(1, sel_launches)
     bytes_per_launch = sel_bytes / max(1, sel_launches)
     achieved = bytes_per_launch / sel_avg_s / 1e9 if sel_avg_s > 0 else 0.0
@@ -297,7 +299,8 @@ def main():
             "dispatches": tw_dispatches,
         },
         "tree_roofline": {
-            "kernel": "k_select<C4> (PUCT tree walk)",
+            "kernel": ("k_select<C4> (PUCT tree walk)" if args.search_threads <= 1 else
+                       f"k_select_vl<C4> (PUCT tree walk, {args.search_threads} sims in flight per tree)"),
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
