@@ -33,7 +33,8 @@ import time
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
-TRAFFIC_FILE = os.path.join(HERE, "profiles", "r01_bench_prof", "k_tower_traffic.json")
+TRAFFIC_FILE = os.path.join(HERE, "profiles", "r01_bench_prof", "k_tower_traffic.json")  # --search-threads 1
+TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r01_bench_prof_k4", "k_tower_traffic.json")  # 4 (default)
 
 # MI355X reference figures (/opt/skills/guides/MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
@@ -247,12 +248,13 @@ def main():
     # WRITE_SIZE passes, scripts/gpu_prof_bench.sh -> scripts/pmc_traffic.py); bench.py cannot run
     # the profiler itself, so it reports the committed measurement for the default workload
     traffic, traffic_src = None, None
-    if os.path.exists(TRAFFIC_FILE) and (args.games, args.sims, args.filter_factor, args.blocks) == (4096, 200, 32, 20):
-        with open(TRAFFIC_FILE) as f:
+    tfile = {1: TRAFFIC_FILE, 4: TRAFFIC_FILE_K4}.get(args.search_threads)
+    if tfile and os.path.exists(tfile) and (args.games, args.sims, args.filter_factor, args.blocks) == (4096, 200, 32, 20):
+        with open(tfile) as f:
             tj = json.load(f)
         # per-dispatch bytes x dispatches per launch (a launch = one simulation step over all lanes)
         traffic = tj.get("bytes_per_dispatch", tj["bytes_per_launch"]) * max(1, args.lanes)
-        traffic_src = os.path.relpath(TRAFFIC_FILE, HERE)
+        traffic_src = os.path.relpath(tfile, HERE)
 
     out = {
         "metric": "self-play positions/sec (Connect4, 200 sims/move)",
