@@ -77,7 +77,7 @@ def g3_tapes(g, threads=1):
     return rec_p.tape, rec_o.tape, (r, moves, log)
 
 
-def g5_tapes(g):
+def g5_tapes(g, threads=1):
     """Per-tree tapes of one G5 evaluation game (policy tree, opposing player)."""
     from oracle.hardcoded import PyRandomRNG
 
@@ -89,7 +89,8 @@ def g5_tapes(g):
     rec_o = RecordingRNG(base if g["opponent"] == "mcts" else PyRandomRNG(g["seed"]))
     # update=True only adds the end-of-game push (no RNG draws): the Moves the arena records
     out = play_episode(g["game"], net_p, net_o, rec_p, rec_o, g["sims"], swap_sides=g["swap_sides"], update=True,
-                       evaluate=True, opponent=g["opponent"], opponent_iterations=g["opponent_sims"] or None)
+                       evaluate=True, opponent=g["opponent"], opponent_iterations=g["opponent_sims"] or None,
+                       threads=threads)
     return rec_p.tape, rec_o.tape, out
 
 
@@ -207,7 +208,7 @@ def run_g3_group(games, leaf_format="f32", leaf_layout="nchw", search_threads=1)
     return merged, counters
 
 
-def run_g5_group(games, record=True):
+def run_g5_group(games, record=True, search_threads=1):
     """Run a group of G5 evaluation games (same game / sims / opponent) as game slots of one
     two-player arena: network-1 rows for a second table net, or hard-coded opponents (tape mode)."""
     import torch
@@ -220,13 +221,14 @@ def run_g5_group(games, record=True):
     game, sims, opp, opp_sims = g0["game"], g0["sims"], g0["opponent"], g0["opponent_sims"]
     G = len(games)
     kind = {"mcts": _lib.PLAYER_MCTS, "lookahead": _lib.PLAYER_LOOKAHEAD, "random": _lib.PLAYER_RANDOM}[opp]
-    arena = Arena(game, n_trees=2 * G, n_games=G, iterations=max(sims, opp_sims), rng="tape", evaluate=True)
+    arena = Arena(game, n_trees=2 * G, n_games=G, iterations=max(sims, opp_sims), rng="tape", evaluate=True,
+                  search_threads=search_threads)
     arena.set_tree_players(nets=[0, 1 if opp == "mcts" else 0] * G, kinds=[_lib.PLAYER_MCTS, kind] * G,
                            budgets=[sims, opp_sims if opp == "mcts" else 0] * G)
     arena.games_set_record(record)
     tapes, oracle = [], []
     for g in games:
-        tp, to, out = g5_tapes(g)
+        tp, to, out = g5_tapes(g, search_threads)
         tapes += [tp, to]
         oracle.append(out)
     arena.set_tapes(tapes)
@@ -255,7 +257,7 @@ def run_g5_group(games, record=True):
         assert n0 + n1 == count
         rows[0] += n0
         rows[1] += n1
-        trees_all = arena.leaf_trees(arena.n_trees)
+        trees_all = arena.leaf_trees(arena.max_rows)
         p0, v0 = seg_eval(0, n0, trees_all)
         p1, v1 = seg_eval(arena.seg1, n1, trees_all)
         arena.expand2(p0, v0, p1, v1)
@@ -265,7 +267,7 @@ def run_g5_group(games, record=True):
         st = arena.games_state()
         plies = np.where(st["state"] == 1, st["ply"], plies)
         arena.games_begin_ply()
-        for _ in range(max(sims, opp_sims)):
+        for _ in range(-(-max(sims, opp_sims) // search_threads)):
             step(arena.select())
         step(arena.games_end_ply())
         fin, ring = arena.games_finish_ply(refill=False)

@@ -267,3 +267,33 @@ def test_threaded_selfplay_games_match_oracle(key, threads):
             q = np.float64(moves["q"][i]) if moves["q_f64"][i] else np.float32(moves["q"][i])
             assert float(q) == float(M["q"]), (gi, i)
     assert np.array_equal(np.array(counters["results"]), exp_results)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", [k for k, _ in _g5_groups()], ids=lambda k: f"{k[0]}-{k[2]}-{k[1]}v{k[3]}")
+def test_threaded_evaluation_games_match_oracle(key):
+    """G5 evaluation games with 4 sims in flight per MCTS tree: two networks in row segments of
+    n_trees * K rows each side of seg1 = n0 * K, per-player budgets cutting the last step;
+    bit-exact vs the oracle's threaded episodes."""
+    from tests.parity_helpers import run_g5_group
+
+    games = dict(_g5_groups())[key]
+    moves, counters, oracle, rows = run_g5_group(games, search_threads=4)
+    assert counters["error_flags"] == 0
+    assert counters["games_finished"] == len(games)
+    exp = np.zeros((2, 3), dtype=np.int64)
+    for g, (r, _, _, _) in zip(games, oracle):
+        exp[int(g["swap_sides"])][{1: 0, 0: 1, -1: 2}[r]] += 1
+    assert np.array_equal(np.array(counters["results"]), exp)
+    by_game = {}
+    for i in range(len(moves["z"])):
+        by_game.setdefault(int(moves["game"][i]), []).append(i)
+    for gi, (g, (r, omoves, log, _)) in enumerate(zip(games, oracle)):
+        got = by_game.get(gi, [])
+        assert len(got) == len(omoves), gi
+        for i, M in zip(got, omoves):
+            assert moves["state"][i].astype(int).tolist() == M["state"].reshape(-1).astype(int).tolist(), (gi, i)
+            assert float(moves["z"][i]) == float(M["actual_val"]), (gi, i)
+            assert moves["tree_probs"][i].astype(float).tolist() == M["tree_probs"].astype(float).tolist(), (gi, i)
+            q = np.float64(moves["q"][i]) if moves["q_f64"][i] else np.float32(moves["q"][i])
+            assert float(q) == float(M["q"]), (gi, i)
