@@ -145,6 +145,7 @@ class SelfPlayScheduler:
         # the reference's workers search with thread_count threads + virtual loss exactly when they
         # talk to an InferenceProxy (mcts.py:154, self_play_parallel.py:95-171): K sims in flight
         threads = int(kw.get("thread_count", 4) or 1) if inference_proxy else 1
+        self._search_threads = max(1, threads)
         ekw = dict(iterations=kw.get("iterations", 100), alpha=kw.get("alpha", 1),
                    strong_play=kw.get("strong_play", False), seed=self.seed + 7919 * self.rank, device=self.device,
                    search_threads=max(1, threads))
@@ -274,7 +275,8 @@ class SelfPlayScheduler:
         return SelfPlayEngine(self.game, self.network, n_games=slots, iterations=kw.get("iterations", 100),
                               alpha=kw.get("alpha", 1), strong_play=kw.get("strong_play", False), evaluate=True,
                               seed=self.seed + 104729 + 7919 * self.rank, device=self.device, opponent=opponent,
-                              opponent_iterations=opp_iters, record=False), per_rank
+                              opponent_iterations=opp_iters, record=False,
+                              search_threads=getattr(self, "_search_threads", 1)), per_rank
 
     def _play_evaluation(self, n_games):
         """n_games evaluation games over all ranks (task i -> swap_sides = i odd, update=False);
@@ -345,6 +347,8 @@ class SelfPlayScheduler:
         Returns (total_rewards, breakdown) exactly as the reference's parse_results."""
         if resume_model:
             self._load_latest(prev_run=True)
+        # evaluation workers talk to the InferenceProxy too: thread_count sims in flight (mcts.py:154)
+        self._search_threads = max(1, int(self._policy_kwargs().get("thread_count", 4) or 1)) if inference_proxy else 1
         reward_list = self._play_evaluation(self.epoch_length)
         return self.parse_results(reward_list)
 
