@@ -107,3 +107,21 @@ def test_host_hardcoded_players_match_oracle(game):
                 orc.play_action(a, p)
             random.seed(case)
             assert host(None) == orc.move(), (case, kind, plays)
+
+
+def test_config_field_offsets_match_header(tmp_path):
+    """ctypes mirror vs the C header (gcc offsetof), incl. search_threads (K sims in flight)."""
+    import os
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    names = [f for f, _ in _lib.Config._fields_]
+    src = tmp_path / "off.c"
+    src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "spmcts.h"\nint main(void){\n' +
+                   "".join(f'printf("%zu\\n", offsetof(spmcts_config, {n}));\n' for n in names) +
+                   'printf("%zu\\n", sizeof(spmcts_config));\nreturn 0;}\n')
+    exe = tmp_path / "off"
+    subprocess.run(["gcc", "-I", os.path.join(root, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    assert got[:-1] == [getattr(_lib.Config, n).offset for n in names]
+    assert got[-1] == ctypes.sizeof(_lib.Config)
