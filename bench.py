@@ -75,7 +75,7 @@ def _cpu_worker(args):
     """One host process: the oracle's sequential search (the reference's MCTreeSearch algorithm,
     numpy RNG) + the reference-architecture ResNet in fp32 torch on ONE thread, Connect4 games
     from the empty board, complete moves only, for `seconds`."""
-    seconds, seed, sims, filter_factor, num_blocks = args
+    seconds, seed, sims, filter_factor, num_blocks, threads = args
     import numpy as np
     import torch
 
@@ -89,7 +89,7 @@ def _cpu_worker(args):
     np.random.seed(seed)
     moves = 0
     with torch.no_grad():
-        tree, env, player = OracleTree("connect4", net, NumpyRNG(), sims), Connect4Env(), 1
+        tree, env, player = OracleTree("connect4", net, NumpyRNG(), sims, threads=threads), Connect4Env(), 1
         t0 = time.time()
         while time.time() - t0 < seconds:
             a = tree.move()
@@ -99,25 +99,27 @@ def _cpu_worker(args):
             player = -player
             if done:
                 env.reset()
-                tree, player = OracleTree("connect4", net, NumpyRNG(), sims), 1
+                tree, player = OracleTree("connect4", net, NumpyRNG(), sims, threads=threads), 1
         dt = time.time() - t0
     return moves, dt
 
 
-def cpu_baseline(seconds, cores, sims, filter_factor, num_blocks):
+def cpu_baseline(seconds, cores, sims, filter_factor, num_blocks, threads=1):
     """The reference's CPU self-play structure restated: `cores` independent play processes (the
     reference runs one SelfPlayWorker per core, self_play_parallel.py:95-171), each running the
     oracle's sequential search with a 1-thread fp32 ResNet, for about `seconds`; positions/s summed
-    over processes.  (No IPC inference batching: the reference's proxy adds queue round trips.)"""
+    over processes.  (No IPC inference batching: the reference's proxy adds queue round trips.)
+    threads > 1: the oracle's threaded (virtual-loss) search, same per-leaf network calls."""
     import multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     with ctx.Pool(cores) as pool:
-        res = pool.map(_cpu_worker, [(seconds, 1000 + i, sims, filter_factor, num_blocks) for i in range(cores)])
+        res = pool.map(_cpu_worker, [(seconds, 1000 + i, sims, filter_factor, num_blocks, threads) for i in range(cores)])
     moves = sum(m for m, _ in res)
     rate = sum(m / dt for m, dt in res)
     return dict(value=rate, unit="positions/s", cores=cores, kind="port",
-                sample=f"{cores} processes x (oracle sequential MCTS, {sims} sims/move, numpy RNG + ResNet-"
+                sample=f"{cores} processes x (oracle MCTS, {sims} sims/move, "
+                       f"{'sequential' if threads <= 1 else f'{threads} sims in flight (virtual loss)'}, numpy RNG + ResNet-"
                        f"{4 * filter_factor}x{num_blocks} fp32 torch, 1 thread), Connect4 games from the empty board, "
                        f"{moves} complete moves in ~{seconds:.0f} s")
 
@@ -152,7 +154,8 @@ def main():
     env_rank, env_world = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
     cpu = None
     if env_rank == 0 and env_world == 1 and not args.no_cpu_baseline and not arena_mode:
-        cpu = cpu_baseline(args.cpu_seconds, min(16, os.cpu_count() or 1), args.sims, args.filter_factor, args.blocks)
+        cpu = cpu_baseline(args.cpu_seconds, min(16, os.cpu_count() or 1), args.sims, args.filter_factor, args.blocks,
+                           threads=args.search_threads)
 
     import torch
 
