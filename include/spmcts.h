@@ -105,6 +105,9 @@ typedef struct spmcts_counters {
   int64_t blocks_in_use_max;   /* peak node blocks used by any tree                          */
   uint32_t error_flags;
   uint32_t reserved;
+  int64_t leaked_sims;         /* threaded mode: sims that found every child invalid or locked and
+                                  ended without a backup, their virtual loss left in place
+                                  (mcts.py:349-354); sims + leaked_sims = searches x iterations */
 } spmcts_counters;
 
 /* ---- library ------------------------------------------------------------ */

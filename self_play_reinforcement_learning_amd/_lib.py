@@ -66,6 +66,7 @@ class Counters(ctypes.Structure):
         ("blocks_in_use_max", ctypes.c_int64),
         ("error_flags", ctypes.c_uint32),
         ("reserved", ctypes.c_uint32),
+        ("leaked_sims", ctypes.c_int64),
     ]
 
     def as_dict(self):

@@ -1944,6 +1944,7 @@ int spmcts_get_counters(spmcts_arena *h, spmcts_counters *out) {
     out->depth_sum += ct[C_DEPTH];
     out->set_node_expansions += ct[C_SETNODE];
     out->moves += ct[C_MOVES];
+    out->leaked_sims += ct[C_LEAK];
   }
   std::vector<int32_t> used(h->v.T);
   HIP_TRY(hipMemcpy(used.data(), h->v.used, 4 * used.size(), hipMemcpyDeviceToHost));

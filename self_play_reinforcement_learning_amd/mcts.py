@@ -52,8 +52,20 @@ class RootView:
         return self.w / self.n if self.n else 0
 
 
-def _mse(a, b):
-    return torch.mean((a.float().view(-1) - b.float().view(-1)) ** 2)
+def az_loss(network, states, actual_val, tree_probs, q, q_average=True):
+    """The AlphaZero loss of MCTreeSearch.loss (mcts.py:234-252) on stacked tensors:
+    MSELossFlat(v, z [+ q]) (rl_utils/flat.py: float targets, mean over the batch) plus
+    -sum(pi * log p) / B.  `states` int64 [B, W, H] in the Move frame (+1 = player to move).
+    Shared by MCTreeSearch.loss and the scheduler's trainer (self_play_parallel._Trainer);
+    pinned by tests/golden/trainer_step.npz (G8)."""
+    dev = next(network.parameters()).device
+    probs, value = network.forward(states.to(dev))
+    z = actual_val.to(dev).float()
+    if q_average:
+        z = z + q.to(dev)
+    value_loss = torch.mean((value.reshape(-1) - z.float().reshape(-1)) ** 2)
+    prob_loss = -(probs.log() * tree_probs.to(dev)).sum() / probs.size()[0]
+    return value_loss + prob_loss
 
 
 class MCTreeSearch(Policy):
@@ -186,16 +198,8 @@ class MCTreeSearch(Policy):
     def loss(self, batch):
         """AlphaZero loss (mcts.py:234-252): MSE(v, z [+ q]) - sum(pi * log p) / B."""
         s, actual_val, tree_probs, q = Move(*zip(*batch))
-        net = self.network
-        dev = next(net.parameters()).device
-        probs, value = net.forward(torch.stack(s).to(dev))
-        z = torch.stack(actual_val).to(dev).float()
-        if self.q_average:
-            z = z + torch.stack(q).to(dev).float()
-        value_loss = _mse(value.view(-1), z)
-        pi = torch.stack(tree_probs).to(dev).float()
-        prob_loss = -(probs.log() * pi).sum() / probs.size()[0]
-        return value_loss + prob_loss
+        return az_loss(self.network, torch.stack(s), torch.stack(actual_val), torch.stack(tree_probs),
+                       torch.stack(q), self.q_average)
 
     def update_from_memory(self):
         if len(self.memory) < self.batch_size:

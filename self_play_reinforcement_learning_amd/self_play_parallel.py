@@ -36,7 +36,7 @@ import torch
 from . import distributed as D
 from .arena import GAMES, game_of_env
 from .engine import LanedEngine, SelfPlayEngine
-from .mcts import MCTreeSearch, Move
+from .mcts import MCTreeSearch, Move, az_loss
 
 
 class LocalQueue:
@@ -116,6 +116,9 @@ class SelfPlayScheduler:
         self.engine = None
         self.trainer = None
         self.epoch_value = 0
+        self._search_threads = 1
+        if policy_container is not None:
+            self._resolve_threads(True)  # the default of every entry point (inference_proxy=True)
         if save_dir and rank == 0:
             os.makedirs(os.path.join(save_dir, self.start_time), exist_ok=True)
 
@@ -136,16 +139,28 @@ class SelfPlayScheduler:
         kw = dict(self.policy_container.policy_kwargs)
         return kw
 
+    def _resolve_threads(self, inference_proxy=True):
+        """Simulations in flight per tree, resolved in one place for self-play and evaluation
+        games: the reference's workers search with thread_count threads + virtual loss exactly when
+        they talk to an InferenceProxy (mcts.py:154, self_play_parallel.py:95-171), which every
+        scheduler entry point does by default.  One arena holds both players, so an evaluation
+        opponent with another thread_count is searched with the policy's (logged)."""
+        k = max(1, int(self._policy_kwargs().get("thread_count", 4) or 1)) if inference_proxy else 1
+        c = self.evaluation_policy_container
+        okw = getattr(c, "policy_kwargs", None) or {}
+        if inference_proxy and c is not None and "thread_count" in okw and max(1, int(okw["thread_count"] or 1)) != k:
+            logging.warning(f"evaluation policy thread_count={okw['thread_count']} differs from the policy's "
+                            f"{k}; the arena searches both sides with {k} simulations in flight")
+        self._search_threads = k
+        return k
+
     def setup_player_workers(self, num_workers=None, inference_proxy=True, threads_per_worker=8, resume_model=False):
         """Build the device self-play engine (replaces the worker processes, :95-171)."""
         kw = self._policy_kwargs()
         n_games = self.n_games or max(64, min(4096, (num_workers or 1) * threads_per_worker * 64))
         if resume_model:
             self._load_latest(prev_run=True)
-        # the reference's workers search with thread_count threads + virtual loss exactly when they
-        # talk to an InferenceProxy (mcts.py:154, self_play_parallel.py:95-171): K sims in flight
-        threads = int(kw.get("thread_count", 4) or 1) if inference_proxy else 1
-        self._search_threads = max(1, threads)
+        threads = self._resolve_threads(inference_proxy)
         ekw = dict(iterations=kw.get("iterations", 100), alpha=kw.get("alpha", 1),
                    strong_play=kw.get("strong_play", False), seed=self.seed + 7919 * self.rank, device=self.device,
                    search_threads=max(1, threads))
@@ -236,9 +251,15 @@ class SelfPlayScheduler:
             D.broadcast_state_dict(self.network)
             self.engine.refresh_network()  # epoch_value reload (selfplayworker.py:109-114)
             self.epoch_value += 1
-            if self.stagger:
+            if self.stagger:  # UpdateWorker.stagger_memory (updateworker.py:107-109)
                 m = self.trainer.memory
                 m.change_size(min(m.max_size + self.stagger_mem_step, 1500000))
+            if self.deduplicate:
+                # updateworker.py:88-89 calls policy.deduplicate() here; with the reference's own Move
+                # that raises TypeError (memory.py:93: the rebuilt tuple lacks q) and, caught, skips the
+                # checkpoint.  The device ring merges duplicate boards (z, tree_probs and q averaged);
+                # its (state, z, tree_probs) part is pinned by G7 (tests/test_memory_golden.py)
+                self.trainer.memory.deduplicate()
             reward = self.evaluate_policy(epoch)
             self.trainer.lr_step(reward)
 
@@ -276,7 +297,7 @@ class SelfPlayScheduler:
                               alpha=kw.get("alpha", 1), strong_play=kw.get("strong_play", False), evaluate=True,
                               seed=self.seed + 104729 + 7919 * self.rank, device=self.device, opponent=opponent,
                               opponent_iterations=opp_iters, record=False,
-                              search_threads=getattr(self, "_search_threads", 1)), per_rank
+                              search_threads=self._search_threads), per_rank
 
     def _play_evaluation(self, n_games):
         """n_games evaluation games over all ranks (task i -> swap_sides = i odd, update=False);
@@ -347,8 +368,7 @@ class SelfPlayScheduler:
         Returns (total_rewards, breakdown) exactly as the reference's parse_results."""
         if resume_model:
             self._load_latest(prev_run=True)
-        # evaluation workers talk to the InferenceProxy too: thread_count sims in flight (mcts.py:154)
-        self._search_threads = max(1, int(self._policy_kwargs().get("thread_count", 4) or 1)) if inference_proxy else 1
+        self._resolve_threads(inference_proxy)  # evaluation workers talk to the InferenceProxy too
         reward_list = self._play_evaluation(self.epoch_length)
         return self.parse_results(reward_list)
 
@@ -357,7 +377,8 @@ class _Trainer:
     """UpdateWorker core (updateworker.py:119-149) on the same device: AZ-loss SGD steps on batches
     sampled from the device replay ring (replay.DeviceReplay), LR on plateau."""
 
-    def __init__(self, network, optim, memory_size, batch_size, min_memory, q_average, device, W=7, H=6, A=7):
+    def __init__(self, network, optim, memory_size, batch_size, min_memory, q_average, device, W=7, H=6, A=7,
+                 train_mode=True):
         from .replay import DeviceReplay
 
         self.network = network
@@ -367,6 +388,7 @@ class _Trainer:
         self.min_memory = min_memory
         self.q_average = q_average
         self.device = device
+        self.train_mode = train_mode  # the UpdateWorker trains in train mode (updateworker.py:63)
         self.scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optim, "max", patience=15, factor=0.5,
                                                                     min_lr=0.00001, cooldown=5)
 
@@ -375,16 +397,16 @@ class _Trainer:
             self.memory.add(queue.get())
 
     def step(self):
+        """One update (mcts.py:254-270): uniform batch without replacement from the device ring."""
         if len(self.memory) < max(self.batch_size, self.min_memory):
             return None
-        self.network.train()
-        s, z, pi, q = self.memory.sample_batch(self.batch_size)  # mcts.py:234-252 on device tensors
-        probs, value = self.network.forward(s)
-        if self.q_average:
-            z = z + q
-        value_loss = torch.mean((value.view(-1) - z) ** 2)
-        prob_loss = -(probs.log() * pi).sum() / probs.size(0)
-        loss = value_loss + prob_loss
+        return self.train_batch(*self.memory.sample_batch(self.batch_size))
+
+    def train_batch(self, s, z, pi, q):
+        """loss (mcts.py:234-252, via mcts.az_loss) -> zero_grad -> backward -> SGD step, with the
+        network in train mode as the UpdateWorker runs it (updateworker.py:63); pinned by G8."""
+        self.network.train(self.train_mode)
+        loss = az_loss(self.network, s, z, pi, q, self.q_average)
         self.optim.zero_grad()
         loss.backward()
         self.optim.step()

@@ -489,6 +489,200 @@ def gen_net_io(ResidualTower, Connect4Env, TicTacToeEnv):
     return out
 
 
+# ----------------------------------------------------------------------------- G7
+def _record_pool(n, n_boards, seed):
+    """n records over n_boards distinct Connect4 boards (so states repeat): int64 [7, 6] state,
+    float32 scalar actual_val in {-1, 0, 1}, float32 [7] tree_probs, float32 scalar q."""
+    rng = np.random.RandomState(seed)
+    boards = []
+    for _ in range(n_boards):
+        b = np.zeros((7, 6), np.int64)
+        h = [0] * 7
+        p = 1
+        for _ in range(rng.randint(0, 12)):
+            c = rng.randint(7)
+            if h[c] < 6:
+                b[c, h[c]] = p
+                h[c] += 1
+                p = -p
+        boards.append(b)
+    pool = []
+    for i in range(n):
+        pool.append(dict(state=boards[rng.randint(n_boards)].reshape(-1).tolist(),
+                         actual_val=float(rng.choice([-1.0, 0.0, 1.0])),
+                         tree_probs=rng.dirichlet([0.7] * 7).astype(np.float32).astype(float).tolist(),
+                         q=float(np.float32(rng.uniform(-1, 1)))))
+    return pool
+
+
+def gen_memory_ops():
+    """The reference's Memory / Deduplicator (rl_utils/memory.py:8-94) driven through a fixed
+    script of operations; every observable result is logged.  Records carry an `id` so that
+    eviction / sampling / ordering can be logged; the key and value fields are tensors exactly as
+    the reference's Move records (mcts.py:282-288, :230)."""
+    from collections import namedtuple
+
+    from games.algos.mcts import Move
+    from rl_utils.memory import Memory
+
+    Rec = namedtuple("Rec", ("state", "actual_val", "tree_probs"))
+    pool = _record_pool(160, 14, seed=7)
+
+    def rec(i, cls=Rec):
+        d = pool[i]
+        f = dict(state=torch.tensor(d["state"], dtype=torch.int64).view(7, 6),
+                 actual_val=torch.tensor(d["actual_val"]).float(),
+                 tree_probs=torch.tensor(d["tree_probs"], dtype=torch.float32))
+        if cls is Move:
+            f["q"] = torch.tensor(d["q"], dtype=torch.float32)
+        r = cls(**f)
+        return r
+
+    def dump(buf):
+        return [dict(state=r.state.reshape(-1).tolist(), actual_val=float(r.actual_val),
+                     tree_probs=[float(x) for x in r.tree_probs.reshape(-1)]) for r in buf]
+
+    ids = {}
+
+    def add(mem, i, cls=Rec):
+        r = rec(i, cls)
+        ids[id(r)] = i
+        mem.add(r)
+
+    log = {}
+    # 1. bounded ring, eviction, sampling, change_size
+    m = Memory(50)
+    for i in range(80):
+        add(m, i)
+    log["ring_after_80"] = [ids[id(r)] for r in m._buffer]
+    np.random.seed(5)
+    log["sample_seed5_k10"] = [ids[id(r)] for r in m.sample(10)]
+    m.change_size(30)
+    log["after_change_size_30"] = [ids[id(r)] for r in m._buffer]
+    log["max_size_after_change"] = m.max_size
+    # 2. deduplicate twice (persistent group table, maxlen rebinding the bound)
+    m.deduplicate("state", ["actual_val", "tree_probs"], Rec)
+    log["dedup1"] = dump(m._buffer)
+    log["max_size_after_dedup1"] = m.max_size
+    for i in range(80, 140):
+        add(m, i)
+    log["len_after_60_more"] = len(m)
+    m.deduplicate("state", ["actual_val", "tree_probs"], Rec, maxlen=9)
+    log["dedup2_maxlen9"] = dump(m._buffer)
+    for i in range(140, 150):
+        add(m, i)
+    log["len_after_10_more"] = len(m)
+    # 3. one-shot dedup of an unbounded memory (the comparison case for DeviceReplay)
+    m2 = Memory()
+    for i in range(120):
+        add(m2, i)
+    m2.deduplicate("state", ["actual_val", "tree_probs"], Rec)
+    log["oneshot_120"] = dump(m2._buffer)
+    # 4. get_duplicates
+    m3 = Memory(100)
+    for i in range(30):
+        add(m3, i)
+    groups, uniq = m3.get_duplicates("state")
+    log["get_duplicates_groups"] = [[int(k), list(v)] for k, v in groups.items()]
+    log["get_duplicates_unique"] = uniq.reshape(len(uniq), -1).tolist()
+    # 5. the reference's own Move through deduplicate (mcts.py:385-386): the rebuilt tuple lacks q
+    m4 = Memory(100)
+    for i in range(40):
+        add(m4, i, Move)
+    try:
+        m4.deduplicate("state", ["actual_val", "tree_probs"], Move)
+        log["move_dedup_error"] = None
+    except Exception as e:  # noqa: BLE001
+        log["move_dedup_error"] = type(e).__name__
+    log["move_dedup_buffer_after"] = dump(m4._buffer)
+    log["move_dedup_len_after"] = len(m4)
+    # 6. reset keeps max_size, empties
+    m.reset()
+    log["len_after_reset"] = len(m)
+    return dict(pool=pool, log=log)
+
+
+# ----------------------------------------------------------------------------- G8
+def gen_trainer_step(ref_mcts, Connect4Env, ResidualTower):
+    """The reference's training step: MCTreeSearch.update_from_memory (mcts.py:254-270) =
+    Memory.sample (np.random.choice, rl_utils/memory.py:26-30) -> MCTreeSearch.loss (mcts.py:234-252,
+    q_average adds the root q) -> SGD(lr, momentum 0.9, weight_decay 1e-4, self_play_parallel.py:193)
+    step, two steps in a row (momentum), on seeded ResidualTower nets.  Modes: "train" (the
+    UpdateWorker's policy.train(), updateworker.py:63: dropout + batch-stat BN, torch seeded per
+    step), "train_nodrop" (the same with both dropout p set to 0: BN batch statistics without the
+    CPU dropout stream, the form a GPU run can reproduce), "eval"."""
+    from rl_utils.memory import Memory
+
+    Move = ref_mcts.Move
+    pool = _record_pool(96, 96, seed=11)
+    out = {}
+    batch_size, lr = 32, 0.01
+    for name, kw, full in (("c4_tiny", dict(num_blocks=1, filter_factor=4), True),
+                           ("c4_128x2", dict(num_blocks=2, filter_factor=32), False)):
+        for mode in ("train", "train_nodrop", "eval"):
+            torch.manual_seed(0)
+            net = ResidualTower(width=7, height=6, action_size=7, **kw)
+            net.eval()
+            init = {k: v.detach().clone() for k, v in net.state_dict().items()}
+            optim = torch.optim.SGD(net.parameters(), lr=lr, momentum=0.9, weight_decay=0.0001)
+            pol = ref_mcts.MCTreeSearch(network=net, env=Connect4Env, optim=optim, batch_size=batch_size,
+                                        memory_size=1000, min_memory=10)
+            pol.memory = Memory(1000)
+            recs = []
+            for d in pool:
+                r = Move(torch.tensor(d["state"], dtype=torch.int64).view(7, 6), torch.tensor(d["actual_val"]).float(),
+                         torch.tensor(d["tree_probs"], dtype=torch.float32), torch.tensor(d["q"], dtype=torch.float32))
+                recs.append(r)
+                pol.memory.add(r)
+            pol.train(mode != "eval")
+            if mode == "train_nodrop":
+                net.policy_dropout.p = 0.0
+                net.value_dropout.p = 0.0
+            losses, picks = [], []
+            orig_loss, orig_sample = pol.loss, pol.memory.sample
+
+            def spy_loss(batch):
+                v = orig_loss(batch)
+                losses.append(float(v))
+                return v
+
+            def spy_sample(k):
+                b = orig_sample(k)
+                picks.append([next(j for j, r in enumerate(recs) if r is x) for x in b])
+                return b
+
+            pol.loss, pol.memory.sample = spy_loss, spy_sample
+            for step in range(2):
+                np.random.seed(100 + step)
+                torch.manual_seed(200 + step)
+                pol.update_from_memory()
+            key = f"{name}/{mode}"
+            out[f"{key}/losses"] = np.array(losses, np.float64)
+            out[f"{key}/picks"] = np.array(picks, np.int64)
+            sd = net.state_dict()
+            names = list(sd.keys())
+            out[f"{key}/keys"] = np.array(names)
+            for stat, fn in (("init_sum", lambda t: init[t].double().sum()),
+                             ("sum", lambda t: sd[t].double().sum()),
+                             ("delta_sum", lambda t: (sd[t].double() - init[t].double()).sum()),
+                             ("delta_l2", lambda t: (sd[t].double() - init[t].double()).norm())):
+                out[f"{key}/{stat}"] = np.array([float(fn(t)) for t in names], np.float64)
+            for t in names:
+                flat = sd[t].reshape(-1)
+                if full:
+                    out[f"{key}/sd/{t}"] = sd[t].numpy()
+                elif flat.numel() and flat.dtype.is_floating_point:
+                    idx = np.unique(np.linspace(0, flat.numel() - 1, 24).astype(np.int64))
+                    out[f"{key}/pick_idx/{t}"] = idx
+                    out[f"{key}/pick_val/{t}"] = flat[torch.from_numpy(idx)].numpy()
+    out["pool/state"] = np.array([d["state"] for d in pool], np.int8)
+    out["pool/actual_val"] = np.array([d["actual_val"] for d in pool], np.float32)
+    out["pool/tree_probs"] = np.array([d["tree_probs"] for d in pool], np.float32)
+    out["pool/q"] = np.array([d["q"] for d in pool], np.float32)
+    out["config"] = np.array([batch_size, lr], np.float64)
+    return out
+
+
 def main():
     ref_mcts, SelfPlayer, Connect4Env, TicTacToeEnv, GameOver, ResidualTower = _ref_imports()
     torch.set_num_threads(4)
@@ -497,6 +691,16 @@ def main():
         print("G5 arena games ...", flush=True)
         with open(os.path.join(HERE, "arena_games.json"), "w") as f:
             json.dump(gen_arena_games(ref_mcts, SelfPlayer, Connect4Env, TicTacToeEnv), f)
+        return
+    if only == ["G7"]:
+        print("G7 memory ops ...", flush=True)
+        with open(os.path.join(HERE, "memory_ops.json"), "w") as f:
+            json.dump(gen_memory_ops(), f)
+        return
+    if only == ["G8"]:
+        print("G8 trainer step ...", flush=True)
+        np.savez_compressed(os.path.join(HERE, "trainer_step.npz"), **gen_trainer_step(ref_mcts, Connect4Env,
+                                                                                       ResidualTower))
         return
     print("G1 env KATs ...", flush=True)
     np.savez_compressed(os.path.join(HERE, "env_kat_c4.npz"), **gen_env_kat_c4(Connect4Env, GameOver))
@@ -514,6 +718,13 @@ def main():
     print("G5 arena games ...", flush=True)
     with open(os.path.join(HERE, "arena_games.json"), "w") as f:
         json.dump(gen_arena_games(ref_mcts, SelfPlayer, Connect4Env, TicTacToeEnv), f)
+    print("G7 memory ops ...", flush=True)
+    with open(os.path.join(HERE, "memory_ops.json"), "w") as f:
+        json.dump(gen_memory_ops(), f)
+    print("G8 trainer step ...", flush=True)
+    np.savez_compressed(os.path.join(HERE, "trainer_step.npz"), **gen_trainer_step(ref_mcts, Connect4Env,
+                                                                                   ResidualTower))
+    print("(G6 threaded-search statistics: tests/golden/make_threaded_stats.py)")
     print("done")
 
 

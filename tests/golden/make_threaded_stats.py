@@ -1,0 +1,239 @@
+"""G6: statistics of the reference's THREADED search, produced by running the reference itself.
+
+Run in the build container only (needs /root/reference):
+
+    python tests/golden/make_threaded_stats.py [table|resnet|resnet_seq|all]
+
+The reference searches with `thread_count` concurrent search_node calls per tree and
+virtual loss whenever its network is an InferenceProxy (games/algos/mcts.py:154,
+:328-331, :340-367) — the default of SelfPlayScheduler.train_model
+(self_play_parallel.py:95-171).  Those threads interleave nondeterministically, so no
+single threaded search can be a bit-exact fixture; what the reference does pin is the
+DISTRIBUTION of search outcomes.  This script reproduces the reference's own serving
+structure, using the reference's classes unchanged:
+
+  * one QueueContainer(threading=threads_per_worker * thread_count) → one InferenceProxy
+    (self_play_parallel.py:102-108);
+  * the reference's InferenceWorker (inference_worker.py:89-119) started as its own
+    process, polling the queues and batching whatever requests are present;
+  * `threads_per_worker` game threads (selfplayworker.py:101-138), each running
+    MCTreeSearch(network=proxy, thread_count=4) searches on fixed positions reached by
+    play_action (mcts.py:188-209), then `_play(1)` (mcts.py:272-299).
+
+Per search it records the Move's tree_probs (the root visit distribution at temperature
+1), the chosen action and the root q.  The GPU test (tests/test_gpu_statistical.py)
+compares the Philox arena's K=4 search against these samples with a stated tolerance.
+
+Sets (200 sims, thread_count 4 unless stated):
+  table_serving / table_single    the deterministic table net (oracle/table_net.py) served
+              through the InferenceWorker, with 8 game threads sharing the worker's queue pool
+              (the reference's default threads_per_worker) or with one game thread;
+  resnet_serving / resnet_single  ResidualTower(7, 6, 7, num_blocks=20, filter_factor=32),
+              random init torch.manual_seed(0) (the bench's ResNet-128x20), same two regimes;
+  resnet_seq  the same net called directly (no proxy: the reference's sequential mode) —
+              the K=1 counterpart at the headline net and budget.
+
+Each position also records how many expansions re-expanded an already expanded node: the
+threaded search checks `is_leaf` before taking the node's lock (mcts.py:357-359), so two
+threads can expand the same leaf and the second replaces the first one's children.  With
+one game thread this is rare; with 8 game threads contending for the GIL it is frequent,
+and it measurably flattens the root visit distribution.
+
+Only inputs and the outputs the reference produced are written (no reference source).
+"""
+import concurrent.futures
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+OUT = os.path.join(HERE, "threaded_stats.json")
+
+sys.path.insert(0, os.path.join(HERE, "refshims"))
+sys.path.insert(0, REF)
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+
+from oracle.table_net import cells_of, table_eval  # noqa: E402
+
+POSITIONS = [[], [3, 3, 2], [2, 4, 3, 3, 1]]
+SIMS = 200
+THREADS = 4          # thread_count (mcts.py:131 default)
+GAME_THREADS = 8     # threads_per_worker (self_play_parallel.py:95 default)
+TABLE_SALT = 4242
+
+
+class TableNetModule(torch.nn.Module):
+    """The table net with the batched `forward(LongTensor[B, W, H]) -> (probs[B, A], v[B, 1])`
+    surface InferenceWorker.calculate expects (inference_worker.py:114-119).  Rows arrive
+    already multiplied by the mover (inference_proxy.py:21-24)."""
+
+    def __init__(self, n_actions, salt):
+        super().__init__()
+        self.n_actions, self.salt = n_actions, salt
+
+    def forward(self, batch):
+        ps, vs = [], []
+        for row in batch.numpy():
+            p, v = table_eval(cells_of(row), self.n_actions, self.salt)
+            ps.append(p)
+            vs.append([v])
+        return torch.tensor(np.array(ps, np.float32)), torch.tensor(np.array(vs, np.float32))
+
+
+def _resnet():
+    from games.general.modules import ResidualTower
+
+    torch.manual_seed(0)
+    net = ResidualTower(width=7, height=6, action_size=7, num_blocks=20, filter_factor=32)
+    net.eval()
+    sd = net.state_dict()
+    return net, {k: float(v.double().sum()) for k, v in sd.items()}
+
+
+def _search_once(MCTreeSearch, Connect4Env, network, opening, thread_count):
+    tree = MCTreeSearch(network=network, env=Connect4Env, iterations=SIMS, thread_count=thread_count)
+    for a in opening:
+        tree.play_action(a, None)
+    tree.train(False)
+    tree.evaluate(False)
+    action = tree()
+    mv = tree.temp_memory[-1]
+    return dict(tree_probs=mv.tree_probs.numpy().astype(float).tolist(), action=int(action), q=float(mv.q),
+                root_n=int(tree.root_node.n))
+
+
+class _ReexpansionCounter:
+    """Observation only: counts MCNode.create_children calls on nodes that already have children.
+    In threaded mode search_node checks `child.is_leaf` before `child.lock.acquire` (mcts.py:357-359),
+    so two threads can both pass the check; the second then re-expands the node, replacing the
+    first thread's children (create_children rebinds `children`, mcts.py:103-107).  How often this
+    happens depends on how the host schedules the threads (GIL contention), so it is recorded."""
+
+    def __init__(self):
+        from games.algos import mcts as ref_mcts
+
+        self.cls, self.orig = ref_mcts.MCNode, ref_mcts.MCNode.create_children
+        self.calls = self.re = 0
+        counter = self
+
+        def wrapped(node, probs, valid):
+            counter.calls += 1
+            if node.children:
+                counter.re += 1
+            return counter.orig(node, probs, valid)
+
+        self.cls.create_children = wrapped
+
+    def close(self):
+        self.cls.create_children = self.orig
+        return dict(expansions=self.calls, re_expansions=self.re)
+
+
+def run_threaded(net_module, samples, label, game_threads):
+    """The reference's serving structure: InferenceWorker process + proxy + game threads."""
+    from games.algos.inference_proxy import InferenceProxy
+    from games.algos.inference_worker import InferenceWorker
+    from games.algos.mcts import MCTreeSearch
+    from games.connect4.connect4env import Connect4Env
+    from rl_utils.queues import QueueContainer
+
+    queue = QueueContainer(threading=game_threads * THREADS)
+    proxy = InferenceProxy(queue.policy_queues)
+    worker = InferenceWorker([queue], net_module, save_dir="/tmp/g6_saves", start_time="g6")
+    worker.daemon = True
+    worker.start()
+    out = []
+    lock = threading.Lock()
+    t0 = time.time()
+    try:
+        for opening in POSITIONS:
+            counter = _ReexpansionCounter()
+            res = []
+
+            def job(_):
+                r = _search_once(MCTreeSearch, Connect4Env, proxy, opening, THREADS)
+                with lock:
+                    res.append(r)
+                    if len(res) % 20 == 0:
+                        print(f"  {label} {opening}: {len(res)}/{samples} ({time.time() - t0:.0f} s)", flush=True)
+
+            with concurrent.futures.ThreadPoolExecutor(game_threads) as ex:
+                list(ex.map(job, range(samples)))
+            out.append(dict(opening=opening, samples=res, **counter.close()))
+    finally:
+        worker.terminate()
+        worker.join()
+    return out
+
+
+def _seq_job(args):
+    opening, seeds = args
+    torch.set_num_threads(1)
+    from games.algos.mcts import MCTreeSearch
+    from games.connect4.connect4env import Connect4Env
+
+    net, _ = _resnet()
+    res = []
+    with torch.no_grad():
+        for s in seeds:
+            np.random.seed(s)
+            res.append(_search_once(MCTreeSearch, Connect4Env, net, opening, 4))  # direct net: sequential
+    return res
+
+
+def run_sequential(samples, procs=8):
+    import multiprocessing as mp
+
+    out = []
+    for pi, opening in enumerate(POSITIONS):
+        seeds = [70_000 + 1000 * pi + i for i in range(samples)]
+        chunks = [(opening, seeds[i::procs]) for i in range(procs)]
+        with mp.get_context("spawn").Pool(procs) as pool:
+            res = [r for part in pool.map(_seq_job, chunks) for r in part]
+        out.append(dict(opening=opening, samples=res))
+        print(f"  resnet_seq {opening}: {len(res)} searches", flush=True)
+    return out
+
+
+def main():
+    torch.multiprocessing.set_start_method("spawn")  # as the reference's entry points (main.py:109)
+    os.chdir("/tmp")  # reference modules may write logs into cwd
+    os.makedirs("/tmp/g6_saves", exist_ok=True)
+    which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    data = json.load(open(OUT)) if os.path.exists(OUT) else {}
+    common = dict(sims=SIMS, thread_count=THREADS, game="connect4")
+    np.random.seed(6)
+    rn = "ResidualTower(7,6,7,num_blocks=20,filter_factor=32) seed 0"
+    for name, gt in (("serving", GAME_THREADS), ("single", 1)):
+        # serving: threads_per_worker game threads share one worker's queue pool, the
+        # reference's default deployment; single: one game thread (its 4 search threads only)
+        if which in ("table", "table_" + name, "all"):
+            torch.set_num_threads(2)
+            data["table_" + name] = dict(common, threads_per_worker=gt, net="table", salt=TABLE_SALT,
+                                         positions=run_threaded(TableNetModule(7, TABLE_SALT), 400,
+                                                                "table_" + name, gt))
+            json.dump(data, open(OUT, "w"))
+        if which in ("resnet", "resnet_" + name, "all"):
+            torch.set_num_threads(6)
+            net, sums = _resnet()
+            data["resnet_" + name] = dict(common, threads_per_worker=gt, net=rn, net_checksums=sums,
+                                          positions=run_threaded(net, 160, "resnet_" + name, gt))
+            json.dump(data, open(OUT, "w"))
+    if which in ("resnet_seq", "all"):
+        _, sums = _resnet()
+        data["resnet_seq"] = dict(common, thread_count=1, threads_per_worker=1, net=rn, net_checksums=sums,
+                                  positions=run_sequential(160))
+        json.dump(data, open(OUT, "w"))
+    print("done")
+
+
+if __name__ == "__main__":
+    main()

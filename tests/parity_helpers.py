@@ -22,6 +22,10 @@ A_OF = {"connect4": 7, "tictactoe": 9}
 CELLS_OF = {"connect4": 42, "tictactoe": 9}
 
 
+def golden_path(name):
+    return os.path.join(GOLDEN, name)
+
+
 def load_json(name):
     with open(os.path.join(GOLDEN, name)) as f:
         return json.load(f)

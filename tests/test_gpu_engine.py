@@ -40,6 +40,9 @@ def test_engine_selfplay_invariants(game, n_games, sims, ff, blocks, threads):
     assert c["error_flags"] == 0
     assert c["games_finished"] == 2 * n_games
     assert c["sims"] > 0 and c["depth_sum"] >= c["sims"]
+    # every search runs exactly `iterations` search_node calls: completed or leaked (mcts.py:349-354)
+    assert c["sims"] + c["leaked_sims"] == sims * c["moves"]
+    assert threads > 1 or c["leaked_sims"] == 0
     moves = {k: np.concatenate([g[k] for g in got]) for k in got[0]}
     assert len(moves["z"]) == c["positions_exported"] == c["moves"]
     assert set(np.unique(moves["z"]).tolist()) <= {-1.0, 0.0, 1.0}

@@ -224,6 +224,7 @@ def test_threaded_search_matches_oracle(key, threads):
     assert counters["error_flags"] == 0
     assert counters["sims"] == sum(e["stats"]["sims"] for _, e in runs)
     assert counters["terminal_leaves"] == sum(e["stats"]["terminal_leaves"] for _, e in runs)
+    assert counters["leaked_sims"] == sum(e["stats"]["leaks"] for _, e in runs)
     for c, (_, e), r in zip(cases, runs, res):
         assert r["child_n"] == e["child_n"], c["id"]
         assert r["child_w"] == e["child_w"], c["id"]

@@ -1,12 +1,12 @@
 """CPU: the device replay ring (self_play_reinforcement_learning_amd/replay.py) against the
 reference Memory semantics (rl_utils/memory.py): deque(maxlen) eviction, uniform sampling without
-replacement, change_size keeping the newest rows, and the Deduplicator's state-keyed averaging."""
+replacement, change_size keeping the newest rows.  Deduplication is pinned against the reference's own
+outputs in test_memory_golden.py."""
 from collections import deque
 
 import numpy as np
 import torch
 
-from self_play_reinforcement_learning_amd.memory import Memory
 from self_play_reinforcement_learning_amd.mcts import Move
 from self_play_reinforcement_learning_amd.replay import DeviceReplay
 
@@ -67,25 +67,3 @@ def test_change_size_keeps_newest():
     np.testing.assert_array_equal(r.z[r._order()].numpy(), m["z"][-8:].numpy())
     r.change_size(30)
     assert len(r) == 8 and r.max_size == 30
-
-
-def test_deduplicate_matches_reference_deduplicator():
-    m = _moves(40, 5, dup_every=3)
-    r = DeviceReplay(100, 7, 6, 7)
-    r.add_moves(m)
-    mem = Memory(100)
-    for i in range(40):
-        mem.add(Move(m["state"][i].long().view(7, 6), m["z"][i], m["tree_probs"][i], torch.tensor(float(m["q"][i]))))
-
-    from collections import namedtuple  # the reference's Deduplicator rebuilds (state, actual_val, tree_probs)
-
-    Rec = namedtuple("Rec", ("state", "actual_val", "tree_probs"))
-    mem.deduplicate("state", ["actual_val", "tree_probs"], Rec)
-    r.deduplicate()
-    ref = list(mem._buffer)
-    assert len(r) == len(ref) < 40
-    live = r._order()
-    for i, rec in enumerate(ref):
-        assert torch.equal(r.state[live[i]].long().view(7, 6), rec.state)
-        assert abs(float(r.z[live[i]]) - float(rec.actual_val)) < 1e-6
-        np.testing.assert_allclose(r.probs[live[i]].numpy(), rec.tree_probs.numpy(), atol=1e-6)
