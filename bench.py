@@ -8,9 +8,10 @@ num_blocks=20, random init, torch.manual_seed(0)), bf16 leaf evaluation.
 A *step* is one ply of every game slot of every rank: 200 PUCT simulations
 (select -> ResNet -> expand/backup) per game, then the move, Move records,
 env step and tree reuse (engine.SelfPlayEngine.ply).  Finished games are
-refilled immediately (steady state); after every ply the episode statistics
-are all-reduced over ranks and finished games' Move records are gathered to
-rank 0 (the replay owner), as in the north star.  Each GPU's games are held in
+refilled immediately (steady state); finished games' Move records are staged
+on each rank's device and, once per episode batch (--exchange-every plies), the
+episode statistics are all-reduced and the records gathered to rank 0 (the
+replay owner), as in the north star.  Each GPU's games are held in
 --lanes arenas (default 2, engine.LanedEngine) on their own HIP streams, so one
 arena's tree kernels run beside the other's ResNet launch.
 
@@ -137,6 +138,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="skip the rank-0 Move gather")
+    ap.add_argument("--exchange-every", type=int, default=8,
+                    help="plies per episode-batch exchange round (Move rows to rank 0 + stats all-reduce)")
     ap.add_argument("--mode", choices=["selfplay", "arena"], default="selfplay")
     ap.add_argument("--lanes", type=int, default=2,
                     help="arenas per GPU on their own HIP streams (engine.LanedEngine); 1 = one arena")
@@ -180,21 +183,20 @@ def main():
     else:
         eng = SelfPlayEngine("connect4", net, n_games=args.games, **kw)
     gathered = []
-
-    def on_moves(m):
-        if not args.no_gather and D.is_distributed():
-            g = D.gather_moves(m, 42, 7)
-            if g is not None:
-                gathered.append(g["z"].shape[0])
-        else:
-            gathered.append(int(m["z"].shape[0]))
+    # finished games' Move rows: staged on each rank's device, gathered to rank 0 once per episode
+    # batch (every --exchange-every plies, and once more at the end of the timed region) together
+    # with the episode statistics (distributed.MoveExchange); a single process hands them on at once
+    ex = D.MoveExchange(42, 7, sink=lambda g: gathered.append(int(g["z"].shape[0])), every=args.exchange_every)
 
     def one_step():
-        eng.ply(on_moves=on_moves if not (args.no_gather or arena_mode) else None)
-        D.all_reduce_stats(eng.stats_vector())  # episode-end statistics exchange
+        eng.ply(on_moves=ex.stage if not (args.no_gather or arena_mode) else None)
+        ex.end_ply(eng.stats_vector)
 
     for _ in range(args.warmup):
         one_step()
+    if D.is_distributed() and args.warmup % args.exchange_every:
+        ex.end_ply(eng.stats_vector, force=True)
+    ex._plies = 0  # the timed region starts a fresh episode batch
     eng.check()
     c0 = eng.counters()
     eng.enable_timers(True)
@@ -206,6 +208,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         one_step()
+    if D.is_distributed() and args.steps % args.exchange_every:
+        ex.end_ply(eng.stats_vector, force=True)  # the rows of the last partial batch reach rank 0 too
     D.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -326,6 +330,7 @@ def main():
             "nn_ms": nn_ms,
             "share_of_step": nn_ms / 1e3 / elapsed if elapsed else None,
         },
+        "exchange": {"every_plies": args.exchange_every, "rounds": ex.rounds, "rows_to_rank0": ex.rows_gathered},
         "tree": {
             "sims": sims_all,
             "mean_select_levels": levels_local / max(1, sims_local),

@@ -102,12 +102,14 @@ typedef struct spmcts_counters {
   int64_t games_finished;
   int64_t positions_exported;  /* Move records exported                                      */
   int64_t results[2][3];       /* [swap_sides][win, draw, loss] (self_play_parallel.py:302-327) */
-  int64_t blocks_in_use_max;   /* peak node blocks used by any tree                          */
+  int64_t blocks_in_use_max;   /* peak node blocks used by any tree (high-water since creation) */
   uint32_t error_flags;
   uint32_t reserved;
   int64_t leaked_sims;         /* threaded mode: sims that found every child invalid or locked and
                                   ended without a backup, their virtual loss left in place
                                   (mcts.py:349-354); sims + leaked_sims = searches x iterations */
+  int64_t compactions;         /* subtree recyclings (node-store compactions before a search; only
+                                  when blocks_per_tree is below the worst case)                 */
 } spmcts_counters;
 
 /* ---- library ------------------------------------------------------------ */

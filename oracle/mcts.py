@@ -21,15 +21,19 @@ active root are never read again, so the restatement stops at the active root
 (observationally equivalent).
 
 Threaded mode (`threads=K > 1`, the reference's `thread_count` search when its
-network is an InferenceProxy, mcts.py:154, :328-331): the reference's threads
-interleave nondeterministically, so the restatement fixes one interleaving —
-each step, K search_node calls select (virtual loss += 1 on the nodes they pass,
-pending leaves locked, terminal leaves backed up at once) before any network
-reply; then the K replies are expanded and backed up in call order, each removing
-its path's virtual loss.  This is the interleaving the HIP arena's k_select_vl /
-k_expand_vl implement.  Parity of this mode is anchored on the reference's
-sequential fixtures (K=1 reduces to them) plus this restatement: the reference
-itself cannot produce a deterministic threaded trace.
+network is an InferenceProxy, mcts.py:154, :328-331): each of the reference's K
+threads runs select -> network wait -> backup and then takes the next
+search_node task, so ~K sims are always in flight and each new select sees the
+other K-1 pending (a rolling window).  Its threads interleave
+nondeterministically, so the restatement fixes the rolling order: K pending
+slots, completed oldest-first (slot order) and each refilled right after its
+backup; a sim that ends without a network call (terminal leaf, backed up at
+once; or a leak, mcts.py:349-354) frees its slot for the next sim at once.
+This is the schedule the HIP arena's k_select_vl / k_expand_vl implement
+(bit-exact on shared tapes).  Against the reference itself it is pinned
+statistically: G6 (tests/golden/threaded_stats.json) holds root visit
+distributions of the reference's own threaded search behind a real
+InferenceProxy / InferenceWorker.
 
 RNG: every random draw goes through an `rng` object with the reference's call
 order: per search one `dirichlet(alpha, A)`, per descended
@@ -250,15 +254,28 @@ class OracleTree:
 
     def search(self):  # mcts.py:323-338
         self._add_noise(self.root)
-        if self.threads > 1:  # mcts.py:328-331
-            done = 0
-            while done < self.iterations:
-                k = min(self.threads, self.iterations - done)
-                pending = [self._select_threaded() for _ in range(k)]
-                for item in pending:
+        if self.threads > 1:  # mcts.py:328-331: thread_count threads over `iterations` tasks
+            slots = [None] * self.threads
+            started = 0
+
+            def fill(j):
+                nonlocal started
+                while started < self.iterations:
+                    started += 1
+                    item = self._select_threaded()
                     if item is not None:
+                        slots[j] = item
+                        return
+
+            for j in range(self.threads):
+                fill(j)
+            while any(x is not None for x in slots):
+                # the network answers every pending leaf; the replies are completed oldest-first
+                for j in range(self.threads):
+                    if slots[j] is not None:
+                        item, slots[j] = slots[j], None
                         self._reply_threaded(*item)
-                done += k
+                    fill(j)
         else:
             for _ in range(self.iterations):
                 self.search_node()

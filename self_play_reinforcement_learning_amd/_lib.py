@@ -67,6 +67,7 @@ class Counters(ctypes.Structure):
         ("error_flags", ctypes.c_uint32),
         ("reserved", ctypes.c_uint32),
         ("leaked_sims", ctypes.c_int64),
+        ("compactions", ctypes.c_int64),
     ]
 
     def as_dict(self):

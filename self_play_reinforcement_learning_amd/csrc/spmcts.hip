@@ -92,6 +92,10 @@ struct View {
   uint64_t *rpos, *rneg;
   int8_t *rplayer;
   int32_t *used;
+  int32_t gc;         // 1: blocks_per_tree below the worst case -> compaction before a search (k_compact)
+  int32_t *gc_list;   // [T][cap] scratch: live blocks (BFS order)
+  int32_t *gc_map;    // [T][cap] scratch: old block -> new block (-1 dead)
+  int32_t *tstarted;  // threaded search: search_node calls started in the current search (inactive: >= limit)
   double *noise;
   uint8_t *noise_on;
   int32_t *pnode;   // [T][MAXD] path node ids (root .. parent of leaf)
@@ -145,7 +149,7 @@ struct View {
   int32_t sim;       // index of the current simulation within the search (by value per launch)
 };
 
-enum { C_SIMS = 0, C_NN = 1, C_TERM = 2, C_DEPTH = 3, C_SETNODE = 4, C_MOVES = 5, C_LEAK = 6, C_NCNT = 8 };
+enum { C_SIMS = 0, C_NN = 1, C_TERM = 2, C_DEPTH = 3, C_SETNODE = 4, C_MOVES = 5, C_LEAK = 6, C_GC = 7, C_HWM = 8, C_NCNT = 10 };
 enum { GS_IDLE = 0, GS_ACTIVE = 1, GS_DONE = 2 };
 
 __device__ __forceinline__ void set_err(const View &v, uint32_t f) { atomicOr(v.err, f); }
@@ -262,6 +266,7 @@ __device__ __forceinline__ void reset_tree(const View &v, int tree, int player, 
   v.rneg[tree] = 0;
   v.rplayer[tree] = (int8_t)player;
   v.noise_on[tree] = 0;
+  v.tstarted[tree] = 0x3fffffff;  // no search in progress
   for (int j = 0; j < v.K; ++j) v.need[(size_t)tree * v.K + j] = 0;
 }
 
@@ -296,6 +301,7 @@ __device__ void draw_noise(const View &v, int tree) {
   }
   for (int j = 0; j < G::A; ++j) v.noise[(size_t)tree * G::APAD + j] = g[j];
   v.noise_on[tree] = 1;
+  v.tstarted[tree] = 0;  // a search begins: `iterations` search_node calls to start
   rng_store(v, tree, r);
 }
 
@@ -322,6 +328,151 @@ __global__ void k_search_begin(View v, const int32_t *trees, int n) {
   v.active[i] = t;
   if (t < 0) return;
   draw_noise<G>(v, t);
+}
+
+// ----------------------------------------------------------------------------
+// kernel: subtree recycling (node-store compaction of one tree before a search)
+// ----------------------------------------------------------------------------
+// The reference keeps every node of a game alive (backup runs to the original root, mcts.py:94-98;
+// its _prune, mcts.py:197-199, is never called), but nothing above the active root is ever read
+// again.  When a tree's remaining blocks cannot hold one more search (iterations + K + 2 blocks:
+// one per network expansion, the _set_node expansion, slack), the blocks still reachable from the
+// active root are slid down to the front of the tree's region, in their old order, and every child
+// index is remapped:
+//   * block 0 slot 0 becomes the root (its record copied there: n, w, p, children, dtype flag, vl);
+//   * the live blocks (BFS from the root's child block, level-synchronous over the workgroup) keep
+//     their relative order, so new index <= old index and the move can run in place, chunk by chunk
+//     (a chunk is read completely before any of it is written);
+//   * the root's child block is the oldest live block (everything below it was allocated after it),
+//     so it lands at block 1 and the relation "child block > parent block" is preserved.
+// Results are unchanged bit for bit (tests run the parity fixtures with a tiny blocks_per_tree).
+// Without an explicit blocks_per_tree the store is sized for the worst case and this never runs.
+template <class G>
+__global__ __launch_bounds__(256) void k_compact(View v, int n_active) {
+  constexpr int P = G::APAD;
+  constexpr int NT = 256;
+  __shared__ int s_head, s_tail, s_carry, s_scan[NT];
+  const int slot = blockIdx.x;
+  if (slot >= n_active) return;
+  const int tree = v.active[slot];
+  if (tree < 0 || !v.gc) return;
+  const int need = min(v.budget[tree], v.iters) + v.K + 2;
+  const int used = v.used[tree];
+  if (v.cap - used >= need) return;
+  const int tid = threadIdx.x;
+  const size_t nb = nbase<G>(v, tree);
+  const size_t bb = (size_t)tree * v.cap;
+  int32_t *list = v.gc_list + bb;
+  int32_t *map = v.gc_map + bb;
+  const int root = v.root[tree];
+  const int croot = v.bc[nb + root];
+  // 1. live blocks: BFS from the root's child block
+  if (tid == 0) {
+    s_head = 0;
+    s_tail = 0;
+    if (croot >= 0) {
+      list[0] = croot;
+      s_tail = 1;
+    }
+  }
+  for (int b = tid; b < used; b += NT) map[b] = -1;
+  __syncthreads();
+  for (;;) {
+    const int head = s_head, tail = s_tail;
+    if (head == tail) break;
+    __syncthreads();
+    for (int k = head * P + tid; k < tail * P; k += NT) {
+      const int blk = list[k / P], j = k % P;
+      const int c = j < G::A ? v.bc[nb + (size_t)blk * P + j] : -1;
+      if (c >= 0) list[atomicAdd(&s_tail, 1)] = c;
+    }
+    __threadfence_block();
+    __syncthreads();
+    if (tid == 0) s_head = tail;
+    __syncthreads();
+  }
+  const int L = s_tail;
+  for (int k = tid; k < L; k += NT) map[list[k]] = 0;
+  __threadfence_block();
+  __syncthreads();
+  // 2. new indices: 1 + rank among the live blocks in old order (block-wide scan in chunks)
+  if (tid == 0) s_carry = 1;
+  __syncthreads();
+  for (int c0 = 0; c0 < used; c0 += NT) {
+    const int b = c0 + tid;
+    const int live = (b < used && map[b] == 0) ? 1 : 0;
+    s_scan[tid] = live;
+    __syncthreads();
+    for (int off = 1; off < NT; off <<= 1) {
+      const int add = tid >= off ? s_scan[tid - off] : 0;
+      __syncthreads();
+      s_scan[tid] += add;
+      __syncthreads();
+    }
+    if (live) map[b] = s_carry + s_scan[tid] - 1;
+    __syncthreads();
+    if (tid == NT - 1) s_carry += s_scan[NT - 1];
+    __syncthreads();
+  }
+  __threadfence_block();
+  __syncthreads();
+  // 3. the root record into block 0 slot 0 (block 0 is never a destination: live blocks map to >= 1)
+  if (tid == 0) {
+    const int32_t rn = v.bn[nb + root];
+    const double rw = v.bw[nb + root];
+    const float rp = v.bp[nb + root];
+    const uint8_t rf = v.bf64[nb + root];
+    const int32_t rvl = v.K > 1 ? v.bvl[nb + root] : 0;
+    v.bn[nb] = rn;
+    v.bw[nb] = rw;
+    v.bp[nb] = rp;
+    v.bf64[nb] = rf;
+    v.bc[nb] = croot >= 0 ? map[croot] : croot;
+    if (v.K > 1) v.bvl[nb] = rvl;
+    v.bvm[bb] = 1u;
+    v.root[tree] = 0;
+  }
+  __threadfence_block();
+  __syncthreads();
+  // 4. slide the live blocks down, chunk by chunk; child indices remapped
+  for (int c0 = 1; c0 < used; c0 += NT / P) {
+    const int b = c0 + tid / P, j = tid % P;
+    const int dst = b < used ? map[b] : -1;
+    int32_t n = 0, c = -1, vl = 0;
+    double w = 0.0;
+    float pr = 0.f;
+    uint8_t f = 0;
+    uint32_t vm = 0;
+    if (dst >= 0) {
+      const size_t i = nb + (size_t)b * P + j;
+      n = v.bn[i];
+      w = v.bw[i];
+      pr = v.bp[i];
+      c = v.bc[i];
+      f = v.bf64[i];
+      if (v.K > 1) vl = v.bvl[i];
+      if (j == 0) vm = v.bvm[bb + b];
+      if (c >= 0) c = map[c];
+    }
+    __syncthreads();
+    if (dst >= 0) {
+      const size_t o = nb + (size_t)dst * P + j;
+      v.bn[o] = n;
+      v.bw[o] = w;
+      v.bp[o] = pr;
+      v.bc[o] = c;
+      v.bf64[o] = f;
+      if (v.K > 1) v.bvl[o] = vl;
+      if (j == 0) v.bvm[bb + dst] = vm;
+    }
+    __threadfence_block();
+    __syncthreads();
+  }
+  if (tid == 0) {
+    v.used[tree] = 1 + L;
+    v.cnt[(size_t)tree * C_NCNT + C_GC] += 1;
+    if (v.cap - (1 + L) < need) set_err(v, SPMCTS_ERR_POOL);  // the live subtree alone fills the store
+  }
 }
 
 // ----------------------------------------------------------------------------
@@ -489,156 +640,190 @@ __global__ __launch_bounds__(64) void k_select(View v, int n_active) {
 }
 
 // ----------------------------------------------------------------------------
-// kernel: select with K simulations in flight per tree (threaded search_node with virtual
-// loss, mcts.py:328-331 / :340-367).  The reference's threads interleave nondeterministically;
-// this kernel fixes the interleaving in which all K threads of a step select before any network
-// reply: sim j of the step walks the tree with the virtual loss of sims 0..j-1 in place (vl += 1
-// on every node it passes, mcts.py:345), sees their pending leaves as locked (score -1e10,
-// mcts.py:86-88, :347), and a terminal leaf is backed up at once with its path's vl removed.  A
-// node whose children are all invalid or locked ends the sim with its vl left in place
-// (mcts.py:349-354).  Pending leaves go to slot tree * K + j; k_expand_vl backs them up in j
-// order.  Locked = child-block index -2 while the leaf waits for the network.
+// threaded search: K simulations in flight per tree with virtual loss (the reference's
+// thread_count search_node calls under an InferenceProxy, mcts.py:154, :328-331, :340-367).
+//
+// The reference's K threads each run select -> wait for the network -> backup, then take the next
+// search_node task, so at any time ~K sims are in flight and a thread's next select sees the other
+// K-1 sims still pending (a ROLLING window).  The arena fixes the order of that rolling schedule:
+// pending slots j = 0..K-1 of a tree are completed in slot order, and each freed slot is refilled
+// right after its backup (FIFO: the oldest pending sim returns first), so every select after the
+// first K sees K-1 pending sims, as with the reference's threads.  One network batch still holds
+// the K pending leaves of every tree.  Sims that end without a network call (a terminal leaf: backed
+// up at once; a leak: every child invalid or locked, mcts.py:349-354, vl left in place) do not
+// occupy a slot: the slot takes the next sim at once, as the reference's thread takes its next task.
+// oracle/mcts.py (OracleTree.search, threads=K) restates exactly this schedule; the G6 fixture
+// (threaded_stats.json) pins its statistics to the reference's own threaded search.
 // ----------------------------------------------------------------------------
+enum { SIM_DONE = 0, SIM_PENDING = 1, SIM_ERROR = -1 };
+
+// One search_node with virtual loss (mcts.py:340-367) for pending slot j of `tree`, run by the
+// tree's P-lane group.  vl += 1 on every node passed (mcts.py:345), children scored with
+// q = (w - vl)/(n + vl) and u = c p sqrt(N + vl_parent)/(1 + n + vl) (mcts.py:59-78), pending leaves
+// locked (child-block index -2, score -1e10, mcts.py:86-88).  Returns SIM_PENDING with the leaf
+// locked and its path stashed in slot j, SIM_DONE for a terminal leaf (backed up, path vl removed)
+// or a leak, SIM_ERROR on a corrupt tree.  The return value is uniform across the group.
+template <class G>
+__device__ int sim_vl(const View &v, int tree, int j, TreeRng &rng, bool &terr, int32_t *s_node, bool noise,
+                      double nz, int64_t *cnt) {
+  constexpr int P = G::APAD;
+  const int lane = threadIdx.x & (P - 1);
+  const int gbase = (threadIdx.x & 63) & ~(P - 1);
+  const size_t nb = nbase<G>(v, tree);
+  const size_t bb = (size_t)tree * v.cap;
+  const int ps = tree * v.K + j;
+  int node = v.root[tree];
+  Board b{v.rpos[tree], v.rneg[tree]};
+  int player = v.rplayer[tree];
+  int node_n = v.bn[nb + node];
+  int node_vl = v.bvl[nb + node] + 1;  // this sim's virtual loss on the node (mcts.py:345)
+  int cb = v.bc[nb + node];
+  int depth = 0;
+  for (;;) {
+    if (lane == 0) {
+      s_node[depth] = node;
+      v.bvl[nb + node] = node_vl;
+    }
+    if (cb < 0) {
+      if (lane == 0) set_err(v, SPMCTS_ERR_STATE);
+      return SIM_ERROR;
+    }
+    const uint32_t vm = v.bvm[bb + cb];
+    const size_t ci = nb + (size_t)cb * P + lane;
+    int cn = 0, cc = -1, cvl = 0;
+    double cw = 0.0;
+    float cp = 0.f;
+    if (lane < G::A) {
+      cn = v.bn[ci];
+      cw = v.bw[ci];
+      cp = v.bp[ci];
+      cc = v.bc[ci];
+      cvl = v.bvl[ci];
+    }
+    // valid (mcts.py:86-88): valid move and not locked by a pending sim
+    const bool valid = (lane < G::A) && ((vm >> lane) & 1u) && cc != -2;
+    double score = -10000000000.0;
+    if (valid) {
+      // q (mcts.py:59-62): (w - vl) / (n + vl)
+      const int ne = cn + cvl;
+      const double q = ne ? (cw - (double)cvl) / (double)ne : 0.0;
+      const double pe = (depth == 0 && noise) ? nz * v.x + (double)cp * (1.0 - v.x) : (double)cp;
+      // u (mcts.py:71-78): sqrt(parent.n + parent.virtual_loss) / (1 + n + virtual_loss)
+      const double u = ((v.cpuct * pe) * sqrt((double)(node_n + node_vl))) / (double)(1 + cn + cvl);
+      score = (player > 0 ? q : -q) + u;
+    }
+    if (!group_or<P>(valid ? 1 : 0)) {  // mcts.py:349-354: return, virtual loss left in place
+      if (lane == 0) cnt[C_LEAK] += 1;
+      return SIM_DONE;
+    }
+    double s = -INFINITY;
+    if (lane < G::A) s = score + 0.000001 * rng_lane(v, rng, lane, &terr);
+    rng_advance(v, rng, G::A);
+    int a = lane;
+    group_argmax<P>(s, a);
+    const int cc_a = __shfl(cc, gbase + a, 64);
+    const int cn_a = __shfl(cn, gbase + a, 64);
+    const int cvl_a = __shfl(cvl, gbase + a, 64);
+    const int child = cb * P + a;
+    if (cc_a < 0) {
+      // leaf: _expand_node (mcts.py:301-321)
+      Board nb2 = b;
+      int rew = 0, done = 0;
+      const int st = step<G>(nb2, a, player, &rew, &done);
+      if (lane == 0) {
+        if (st != STEP_OK) set_err(v, SPMCTS_ERR_STATE);
+        cnt[C_SIMS] += 1;
+        cnt[C_DEPTH] += depth + 1;
+        if (done) {
+          // terminal: backup (mcts.py:94-98) then remove the path's virtual loss (:365)
+          const double val = terminal_value(v, b, rew * player);
+          v.bn[nb + child] += 1;
+          v.bw[nb + child] += val;
+          if (v.strong) v.bf64[nb + child] = 1;
+          for (int k = 0; k <= depth; ++k) {
+            const size_t idx = nb + s_node[k];
+            v.bn[idx] += 1;
+            v.bw[idx] += val;
+            if (v.strong) v.bf64[idx] = 1;
+            v.bvl[idx] -= 1;
+          }
+          cnt[C_TERM] += 1;
+        } else {
+          // lock the leaf (mcts.py:359) and stash the path for the backup
+          v.bc[nb + child] = -2;
+          const size_t pb = (size_t)ps * G::MAXD;
+          for (int k = 0; k <= depth; ++k) v.pnode[pb + k] = s_node[k];
+          v.plen[ps] = depth + 1;
+          v.leaf[ps] = child;
+          v.lpos[ps] = nb2.pos;
+          v.lneg[ps] = nb2.neg;
+          v.lmover[ps] = (int8_t)player;
+          v.need[ps] = 1;
+        }
+      }
+      return done ? SIM_DONE : SIM_PENDING;
+    }
+    play<G>(b, a, player);
+    node = child;
+    node_n = cn_a;
+    node_vl = cvl_a + 1;
+    cb = cc_a;
+    player = -player;
+    ++depth;
+    if (depth >= G::MAXD) {
+      if (lane == 0) set_err(v, SPMCTS_ERR_STATE);
+      return SIM_ERROR;
+    }
+  }
+}
+
+// Refill pending slot j: start sims until one waits for the network or the tree's budget of
+// search_node calls is spent (`started` counts them, mcts.py:328-331 submits `iterations`).
+template <class G>
+__device__ int fill_slot_vl(const View &v, int tree, int j, int limit, int &started, TreeRng &rng, bool &terr,
+                            int32_t *s_node, bool noise, double nz, int64_t *cnt) {
+  while (started < limit) {
+    ++started;
+    const int r = sim_vl<G>(v, tree, j, rng, terr, s_node, noise, nz, cnt);
+    // the next sim reads what this one wrote (lane 0's stores, other lanes' loads): one wave owns
+    // the tree, so a workgroup-scope fence (stores complete, same CU's L1) is enough
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    if (r != SIM_DONE) return r;
+  }
+  return SIM_DONE;
+}
+
+// First step of a search: fill the K slots of every searching tree.
 template <class G>
 __global__ __launch_bounds__(64) void k_select_vl(View v, int n_active) {
   constexpr int P = G::APAD;
   constexpr int GPB = 64 / P;
   __shared__ int32_t s_node[GPB][G::MAXD];
-
   const int lane = threadIdx.x & (P - 1);
   const int grp = threadIdx.x / P;
   const int slot = blockIdx.x * GPB + grp;
   if (slot >= n_active) return;
   const int tree = v.active[slot];
   if (tree < 0) return;
-
-  const size_t nb = nbase<G>(v, tree);
-  const size_t bb = (size_t)tree * v.cap;
+  const int limit = min(v.budget[tree], v.iters);
+  int started = v.tstarted[tree];
+  if (started >= limit) return;
   const bool noise = v.noise_on[tree] != 0;
   const double nz = (noise && lane < G::A) ? v.noise[(size_t)tree * P + lane] : 0.0;
-  const int gbase = (threadIdx.x & 63) & ~(P - 1);
   TreeRng rng;
   rng_load(v, tree, rng);
   bool terr = false;
   int64_t *cnt = v.cnt + (size_t)tree * C_NCNT;
-
-  const int limit = min(v.budget[tree], v.iters);
   for (int j = 0; j < v.K; ++j) {
-    if (v.sim + j >= limit) break;
-    const int ps = tree * v.K + j;
-    int node = v.root[tree];
-    Board b{v.rpos[tree], v.rneg[tree]};
-    int player = v.rplayer[tree];
-    int node_n = v.bn[nb + node];
-    int node_vl = v.bvl[nb + node] + 1;  // this sim's virtual loss on the node (mcts.py:345)
-    int cb = v.bc[nb + node];
-    int depth = 0;
-    for (;;) {
-      if (lane == 0) {
-        s_node[grp][depth] = node;
-        v.bvl[nb + node] = node_vl;
-      }
-      if (cb < 0) {
-        if (lane == 0) set_err(v, SPMCTS_ERR_STATE);
-        return;
-      }
-      const uint32_t vm = v.bvm[bb + cb];
-      const size_t ci = nb + (size_t)cb * P + lane;
-      int cn = 0, cc = -1, cvl = 0;
-      double cw = 0.0;
-      float cp = 0.f;
-      if (lane < G::A) {
-        cn = v.bn[ci];
-        cw = v.bw[ci];
-        cp = v.bp[ci];
-        cc = v.bc[ci];
-        cvl = v.bvl[ci];
-      }
-      // valid (mcts.py:86-88): valid move and not locked by a pending sim
-      const bool valid = (lane < G::A) && ((vm >> lane) & 1u) && cc != -2;
-      double score = -10000000000.0;
-      if (valid) {
-        // q (mcts.py:59-62): (w - vl) / (n + vl)
-        const int ne = cn + cvl;
-        const double q = ne ? (cw - (double)cvl) / (double)ne : 0.0;
-        const double pe = (depth == 0 && noise) ? nz * v.x + (double)cp * (1.0 - v.x) : (double)cp;
-        // u (mcts.py:71-78): sqrt(parent.n + parent.virtual_loss) / (1 + n + virtual_loss)
-        const double u = ((v.cpuct * pe) * sqrt((double)(node_n + node_vl))) / (double)(1 + cn + cvl);
-        score = (player > 0 ? q : -q) + u;
-      }
-      if (!group_or<P>(valid ? 1 : 0)) {  // mcts.py:349-354: return, virtual loss left in place
-        if (lane == 0) cnt[C_LEAK] += 1;
-        break;
-      }
-      double s = -INFINITY;
-      if (lane < G::A) s = score + 0.000001 * rng_lane(v, rng, lane, &terr);
-      rng_advance(v, rng, G::A);
-      int a = lane;
-      group_argmax<P>(s, a);
-      const int cc_a = __shfl(cc, gbase + a, 64);
-      const int cn_a = __shfl(cn, gbase + a, 64);
-      const int cvl_a = __shfl(cvl, gbase + a, 64);
-      const int child = cb * P + a;
-      if (cc_a < 0) {
-        // leaf: _expand_node (mcts.py:301-321)
-        Board nb2 = b;
-        int rew = 0, done = 0;
-        const int st = step<G>(nb2, a, player, &rew, &done);
-        if (lane == 0) {
-          if (st != STEP_OK) set_err(v, SPMCTS_ERR_STATE);
-          cnt[C_SIMS] += 1;
-          cnt[C_DEPTH] += depth + 1;
-          if (done) {
-            // terminal: backup (mcts.py:94-98) then remove the path's virtual loss (:365)
-            const double val = terminal_value(v, b, rew * player);
-            v.bn[nb + child] += 1;
-            v.bw[nb + child] += val;
-            if (v.strong) v.bf64[nb + child] = 1;
-            for (int k = 0; k <= depth; ++k) {
-              const size_t idx = nb + s_node[grp][k];
-              v.bn[idx] += 1;
-              v.bw[idx] += val;
-              if (v.strong) v.bf64[idx] = 1;
-              v.bvl[idx] -= 1;
-            }
-            cnt[C_TERM] += 1;
-          } else {
-            // lock the leaf (mcts.py:359) and stash the path for k_expand_vl
-            v.bc[nb + child] = -2;
-            const size_t pb = (size_t)ps * G::MAXD;
-            for (int k = 0; k <= depth; ++k) v.pnode[pb + k] = s_node[grp][k];
-            v.plen[ps] = depth + 1;
-            v.leaf[ps] = child;
-            v.lpos[ps] = nb2.pos;
-            v.lneg[ps] = nb2.neg;
-            v.lmover[ps] = (int8_t)player;
-            v.need[ps] = 1;
-          }
-        }
-        break;
-      }
-      play<G>(b, a, player);
-      node = child;
-      node_n = cn_a;
-      node_vl = cvl_a + 1;
-      cb = cc_a;
-      player = -player;
-      ++depth;
-      if (depth >= G::MAXD) {
-        if (lane == 0) set_err(v, SPMCTS_ERR_STATE);
-        return;
-      }
-    }
-    // the next sim reads what this one wrote (lane 0's stores, other lanes' loads): one wave owns
-    // the tree, so a workgroup-scope fence (stores complete, same CU's L1) is enough
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    if (v.need[tree * v.K + j]) continue;
+    if (fill_slot_vl<G>(v, tree, j, limit, started, rng, terr, s_node[grp], noise, nz, cnt) == SIM_ERROR) return;
   }
   if (lane == 0) {
+    v.tstarted[tree] = started;
     if (terr) set_err(v, SPMCTS_ERR_TAPE);
     rng_store(v, tree, rng);
   }
 }
-
 // ----------------------------------------------------------------------------
 // kernel: compaction of pending leaves into rows (tree order => deterministic)
 // ----------------------------------------------------------------------------
@@ -787,24 +972,41 @@ __global__ __launch_bounds__(64) void k_expand(View v, const float *probs0, cons
     v.used[tree] = blk + 1;
     v.need[tree] = 0;
     v.cnt[(size_t)tree * C_NCNT + C_NN] += 1;
+    v.cnt[(size_t)tree * C_NCNT + C_HWM] = max(v.cnt[(size_t)tree * C_NCNT + C_HWM], (int64_t)(blk + 1));
   }
 }
 
 // ----------------------------------------------------------------------------
-// kernel: expand + backup of the K pending leaves of each tree, in in-flight order j (the
-// replies of the threaded search, mcts.py:360-365): create_children, backup (n += 1, w += v on
-// the leaf and its path), unlock, vl -= 1 on the path.  Read-modify-write: earlier slots of the
-// same tree have changed the shared ancestors.
+// kernel: the network replies of the threaded search, slot by slot (mcts.py:360-365): create_children,
+// backup (n += 1, w += v on the leaf and its path), unlock, vl -= 1 on the path — and, while the
+// search has sims left, refill the slot at once (the rolling schedule above).  Read-modify-write:
+// earlier slots of the same tree have changed the shared ancestors.  Pending leaves of trees that
+// are not searching (a _set_node expansion, slot 0, path length 0) are completed without a refill.
 // ----------------------------------------------------------------------------
 template <class G>
 __global__ __launch_bounds__(64) void k_expand_vl(View v, const float *probs0, const float *values0,
                                                   const float *probs1, const float *values1) {
   constexpr int P = G::APAD;
+  constexpr int GPB = 64 / P;
+  __shared__ int32_t s_node[GPB][G::MAXD];
   const int lane = threadIdx.x & (P - 1);
+  const int grp = threadIdx.x / P;
   const int tree = (blockIdx.x * blockDim.x + threadIdx.x) / P;
   if (tree >= v.T) return;
   const size_t nb = nbase<G>(v, tree);
   const size_t bb = (size_t)tree * v.cap;
+  const int limit = min(v.budget[tree], v.iters);
+  int started = v.tstarted[tree];
+  const bool refill = started < limit;
+  bool any = false;
+  for (int j = 0; j < v.K; ++j) any = any || v.need[tree * v.K + j];
+  if (!any) return;
+  const bool noise = v.noise_on[tree] != 0;
+  const double nz = (noise && lane < G::A) ? v.noise[(size_t)tree * P + lane] : 0.0;
+  TreeRng rng;
+  if (refill) rng_load(v, tree, rng);
+  bool terr = false;
+  int64_t *cnt = v.cnt + (size_t)tree * C_NCNT;
   for (int j = 0; j < v.K; ++j) {
     const int ps = tree * v.K + j;
     if (!v.need[ps]) continue;
@@ -844,8 +1046,16 @@ __global__ __launch_bounds__(64) void k_expand_vl(View v, const float *probs0, c
       v.used[tree] = blk + 1;
       v.need[ps] = 0;
       v.cnt[(size_t)tree * C_NCNT + C_NN] += 1;
+      v.cnt[(size_t)tree * C_NCNT + C_HWM] = max(v.cnt[(size_t)tree * C_NCNT + C_HWM], (int64_t)(blk + 1));
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    if (refill && fill_slot_vl<G>(v, tree, j, limit, started, rng, terr, s_node[grp], noise, nz, cnt) == SIM_ERROR)
+      return;
+  }
+  if (refill && lane == 0) {
+    v.tstarted[tree] = started;
+    if (terr) set_err(v, SPMCTS_ERR_TAPE);
+    rng_store(v, tree, rng);
   }
 }
 
@@ -1412,6 +1622,9 @@ static void plan_arena(spmcts_arena *h, Plan &pl) {
   pl.add(&v.rneg, T);
   pl.add(&v.rplayer, T);
   pl.add(&v.used, T);
+  pl.add(&v.gc_list, v.gc ? T * cap : 1);
+  pl.add(&v.gc_map, v.gc ? T * cap : 1);
+  pl.add(&v.tstarted, T);
   pl.add(&v.noise, T * P);
   pl.add(&v.noise_on, T);
   const size_t NS = v.NS;  // pending slots
@@ -1481,6 +1694,7 @@ static int setup_view(spmcts_arena *h, const spmcts_config *cfg) {
   v.G = cfg->n_games;
   v.A = A;
   v.cap = cfg->blocks_per_tree > 0 ? cfg->blocks_per_tree : default_cap(cfg, cells);
+  v.gc = v.cap < default_cap(cfg, cells) ? 1 : 0;  // below the worst case: recycle subtrees (k_compact)
   v.cpuct = cfg->cpuct;
   v.x = cfg->x_noise;
   v.alpha = cfg->alpha;
@@ -1513,6 +1727,7 @@ __global__ void k_rng_init(View v, uint64_t seed, uint64_t sub0) {
   v.tape_cur[t] = 0;
   ((int64_t *)v.tape_end)[t] = 0;
   for (int j = 0; j < v.K; ++j) v.need[(size_t)t * v.K + j] = 0;
+  v.tstarted[t] = 0x3fffffff;
   v.noise_on[t] = 0;
   v.tnet[t] = 0;
   v.tkind[t] = SPMCTS_PLAYER_MCTS;
@@ -1682,6 +1897,7 @@ int spmcts_search_begin(spmcts_arena *h, const int32_t *trees_dev, int32_t n, sp
   if (n <= 0) return 0;
   DISPATCH(h, hipLaunchKernelGGL(k_search_begin<GG>, dim3(nblk(n, 128)), dim3(128), 0, (hipStream_t)stream, h->v,
                                  trees_dev, n));
+  if (h->v.gc) DISPATCH(h, hipLaunchKernelGGL(k_compact<GG>, dim3(n), dim3(256), 0, (hipStream_t)stream, h->v, n));
   LAUNCH_CHECK();
   return 0;
 }
@@ -1886,6 +2102,8 @@ int spmcts_games_begin_ply(spmcts_arena *h, spmcts_stream stream) {
   h->v.sim = 0;
   DISPATCH(h, hipLaunchKernelGGL(k_games_begin_ply<GG>, dim3(nblk(h->v.G, 128)), dim3(128), 0, (hipStream_t)stream,
                                  h->v));
+  if (h->v.gc)
+    DISPATCH(h, hipLaunchKernelGGL(k_compact<GG>, dim3(h->v.G), dim3(256), 0, (hipStream_t)stream, h->v, h->v.G));
   LAUNCH_CHECK();
   return 0;
 }
@@ -1945,6 +2163,8 @@ int spmcts_get_counters(spmcts_arena *h, spmcts_counters *out) {
     out->set_node_expansions += ct[C_SETNODE];
     out->moves += ct[C_MOVES];
     out->leaked_sims += ct[C_LEAK];
+    out->compactions += ct[C_GC];
+    out->blocks_in_use_max = std::max<int64_t>(out->blocks_in_use_max, ct[C_HWM]);
   }
   std::vector<int32_t> used(h->v.T);
   HIP_TRY(hipMemcpy(used.data(), h->v.used, 4 * used.size(), hipMemcpyDeviceToHost));

@@ -1,4 +1,4 @@
-"""Multi-GPU self-play: one process per GPU, games sharded, RCCL only at episode end.
+"""Multi-GPU self-play: one process per GPU, games sharded, RCCL only at episode-batch ends.
 
 The reference's only parallelism is CPU processes exchanging every leaf over
 multiprocessing queues (games/algos/self_play_parallel.py:95-171,
@@ -7,13 +7,16 @@ weights within an epoch), so here every rank owns its own arena of game slots
 and its own Philox subsequences (subsequence0 = rank * n_trees) and the data
 path has no collective.  The exchange steps are the ones the reference has:
 
-  * episode statistics (games finished, wins/draws/losses by side) are summed
-    over ranks — `all_reduce(SUM)` of an int64[8] per ply
-    (self_play_parallel.py:302-327 parse_results, result_queue);
   * finished games' Move records go to the replay owner on rank 0
     (memory_queue -> UpdateWorker -> Memory, mcts.py:225-232,
-    updateworker.py:119-125): all_gather of per-rank counts, then of the
-    records packed into fixed-size byte rows;
+    updateworker.py:119-125) and episode statistics (games finished,
+    wins/draws/losses by side, self_play_parallel.py:302-327) are summed over
+    ranks — both in ONE exchange round per episode batch (`MoveExchange`: every
+    `every` plies and at the end of a run).  Between rounds each rank stages
+    its finished games' packed Move rows on its own device; a round is one
+    all_gather of a small int64 header per rank (row count, not-done flag,
+    stats) and one `gather` of the padded rows to rank 0, where they are
+    unpacked on the device and handed to the sink (the device replay ring);
   * weights are broadcast from rank 0 at epoch boundaries (the reference's
     checkpoint reload, selfplayworker.py:109-114).
 
@@ -125,11 +128,12 @@ def pack_moves(moves):
 
 
 def unpack_moves(rows, cells, n_actions):
+    """uint8 [n, row_bytes] -> dict of per-record tensors, on the rows' device."""
     widths = {"state": cells, "tree_probs": 4 * n_actions, "q": 8, "q_f64": 1, "z": 4, "game": 8}
     out, off = {}, 0
     for name, dt in _FIELDS:
         w = widths[name]
-        chunk = torch.empty((rows.shape[0], w), dtype=torch.uint8).copy_(rows[:, off:off + w])  # fresh, offset 0
+        chunk = torch.empty((rows.shape[0], w), dtype=torch.uint8, device=rows.device).copy_(rows[:, off:off + w])
         t = chunk.view(dt)
         out[name] = t if name in ("state", "tree_probs") else t.reshape(-1)
         off += w
@@ -156,6 +160,75 @@ def gather_moves(moves, cells, n_actions, dst=0):
         return None
     allrows = torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0).cpu()
     return unpack_moves(allrows, cells, n_actions)
+
+
+def row_bytes(cells, n_actions):
+    return cells + 4 * n_actions + 8 + 1 + 4 + 8
+
+
+class MoveExchange:
+    """Episode-batch exchange of Move records and statistics (rank `dst` owns the replay).
+
+    `stage(moves)` is the engines' per-ply on_moves callback: without a process group it hands the
+    records straight to `sink`; with one it only packs them into device rows (no collective, no
+    host synchronisation).  `end_ply(stats_fn, done)` runs an exchange round every `every` plies
+    (or when `force`): one all_gather of an int64 header [rows, not-done, stats...] per rank, then
+    one gather of the rows padded to the largest count, to `dst` only.  On `dst` the rows are
+    unpacked on the device and passed to `sink`.  It returns None on plies without a round, else
+    (all ranks done, stats summed over ranks), so loops that end on it stay in step.
+    """
+
+    def __init__(self, cells, n_actions, sink=None, every=8, dst=0):
+        self.cells, self.A, self.sink, self.every, self.dst = cells, n_actions, sink, max(1, int(every)), dst
+        self.width = row_bytes(cells, n_actions)
+        self._staged = []
+        self._plies = 0
+        self.rounds = 0
+        self.rows_gathered = 0
+
+    def stage(self, moves):
+        if not is_distributed():
+            n = int(moves["z"].shape[0])
+            self.rows_gathered += n
+            if self.sink is not None and n:
+                self.sink(moves)
+            return
+        if int(moves["z"].shape[0]):
+            self._staged.append(pack_moves(moves))
+
+    def end_ply(self, stats_fn=None, done=False, force=False):
+        self._plies += 1
+        if not is_distributed():  # nothing to exchange; the local statistics are the engine's counters
+            return bool(done), None
+        if not force and self._plies % self.every:
+            return None
+        return self.exchange(stats_fn() if stats_fn is not None else [], done)
+
+    def exchange(self, stats, done):
+        dev = _comm_device()
+        world = dist.get_world_size()
+        rows = torch.cat(self._staged, 0).to(dev) if self._staged else torch.zeros((0, self.width), dtype=torch.uint8,
+                                                                                  device=dev)
+        self._staged = []
+        head = torch.tensor([rows.shape[0], 0 if done else 1] + [int(x) for x in stats], dtype=torch.int64, device=dev)
+        heads = [torch.zeros_like(head) for _ in range(world)]
+        dist.all_gather(heads, head)
+        h = torch.stack(heads).cpu()
+        counts = h[:, 0].tolist()
+        all_done = int(h[:, 1].sum()) == 0
+        mx = max(counts)
+        if mx:
+            pad = torch.zeros((mx, self.width), dtype=torch.uint8, device=dev)
+            pad[: rows.shape[0]] = rows
+            bufs = [torch.zeros_like(pad) for _ in range(world)] if dist.get_rank() == self.dst else None
+            dist.gather(pad, gather_list=bufs, dst=self.dst)
+            if bufs is not None:
+                allrows = torch.cat([b[:c] for b, c in zip(bufs, counts) if c], 0)
+                self.rows_gathered += int(allrows.shape[0])
+                if self.sink is not None:
+                    self.sink(unpack_moves(allrows, self.cells, self.A))
+        self.rounds += 1
+        return all_done, h[:, 2:].sum(0).tolist()
 
 
 def broadcast_state_dict(module, src=0):

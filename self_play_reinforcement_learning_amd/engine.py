@@ -278,9 +278,6 @@ class SelfPlayEngine:
             exported = int(moves["z"].shape[0])
             if on_moves is not None:
                 on_moves(moves)
-        elif on_moves is not None and distributed.is_distributed():
-            # every rank takes part in the per-ply collectives in on_moves, with or without records
-            on_moves(a.export_moves(0))
         self.games_done += finished
         self.positions += exported
         self.plies += 1
@@ -307,22 +304,34 @@ class SelfPlayEngine:
                 break
         return dict(plies=n, seconds=time.time() - t0, games=self.games_done, positions=self.positions)
 
-    def play_games(self, n, on_moves=None, on_ply=None):
+    def play_games(self, n, on_moves=None, on_ply=None, exchange=None, every=8):
         """Play exactly `n` more games (refilling slots on device until n have started).
 
         Returns the number of plies it took.  Game ids continue from earlier calls, so
         swap_sides alternates across calls exactly as the reference's task ids do.
-        Under torch.distributed every rank plays its own `n` and keeps stepping (idle plies)
-        until all ranks are done, so the per-ply collectives in on_moves / on_ply stay matched."""
+        Finished games' Move records reach `on_moves` through a distributed.MoveExchange: at once
+        in a single process; under torch.distributed batched to rank 0 every `every` plies (the
+        episode-batch exchange), where every rank plays its own `n` and keeps stepping idle plies
+        until an exchange round finds all ranks done, so the collectives stay matched."""
         target = self._play_games_setup(n)
+        if n <= 0 and not distributed.is_distributed():
+            return 0
+        ex = exchange if exchange is not None else distributed.MoveExchange(*self._record_shape(), sink=on_moves,
+                                                                            every=every)
         plies = 0
-        while not distributed.all_ranks_true(self.games_done >= target):
-            self.ply(on_moves=on_moves)
+        while True:
+            self.ply(on_moves=ex.stage)
             plies += 1
             if on_ply is not None:
                 on_ply(self)
+            r = ex.end_ply(self.stats_vector, done=self.games_done >= target)
+            if r is not None and r[0]:
+                break
         self._started = self._limit
         return plies
+
+    def _record_shape(self):
+        return self.arena.cells, self.arena.A
 
     def _play_games_setup(self, n):
         """Raise the game budget by `n` and start idle slots; returns the games_done target."""
@@ -499,8 +508,8 @@ class LanedEngine:
                 break
         return dict(plies=n, seconds=time.time() - t0, games=self.games_done, positions=self.positions)
 
-    def play_games(self, n, on_moves=None, on_ply=None):
-        """As SelfPlayEngine.play_games, the n games split over the lanes."""
+    def play_games(self, n, on_moves=None, on_ply=None, exchange=None, every=8):
+        """As SelfPlayEngine.play_games, the n games split over the lanes (one exchange for all lanes)."""
         self._lanes_wait_caller()
         k = len(self.lanes)
         parts = [n // k + (1 if i < n % k else 0) for i in range(k)]
@@ -508,12 +517,19 @@ class LanedEngine:
         for e, st, m in zip(self.lanes, self.streams, parts):
             with torch.cuda.stream(st):
                 targets.append(e._play_games_setup(m))
+        if n <= 0 and not distributed.is_distributed():
+            return 0
+        ex = exchange if exchange is not None else distributed.MoveExchange(*self.lanes[0]._record_shape(),
+                                                                            sink=on_moves, every=every)
         plies = 0
-        while not distributed.all_ranks_true(all(e.games_done >= t for e, t in zip(self.lanes, targets))):
-            self.ply(on_moves=on_moves)
+        while True:
+            self.ply(on_moves=ex.stage)
             plies += 1
             if on_ply is not None:
                 on_ply(self)
+            r = ex.end_ply(self.stats_vector, done=all(e.games_done >= t for e, t in zip(self.lanes, targets)))
+            if r is not None and r[0]:
+                break
         for e in self.lanes:
             e._started = e._limit
         return plies

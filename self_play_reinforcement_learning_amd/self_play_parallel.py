@@ -82,7 +82,7 @@ class SelfPlayScheduler:
     def __init__(self, policy_container, env, evaluation_policy_container=None, network=None, swap_sides=True,
                  save_dir="saves", epoch_length=500, initial_games=64, lr=0.001, stagger=False, evaluation_games=100,
                  evaluation_network=None, stagger_mem_step=5000, deduplicate=False, update_delay=0.01,
-                 self_play=None, n_games=None, device=None, seed=0, updates_per_ply=4, lanes=None):
+                 self_play=None, n_games=None, device=None, seed=0, updates_per_ply=4, lanes=None, exchange_every=8):
         self.policy_container = policy_container
         self.evaluation_policy_container = evaluation_policy_container
         self.env_gen = env
@@ -102,6 +102,7 @@ class SelfPlayScheduler:
         self.network = self._get_network(network, policy_container)
         self.seed = seed
         self.updates_per_ply = updates_per_ply
+        self.exchange_every = exchange_every  # plies per episode-batch exchange round (distributed.MoveExchange)
         # >1: LanedEngine (arenas on separate HIP streams, each a complete arena); None = 2 lanes for
         # arenas of >= 1,024 games, where the overlap pays (bench.py), else one arena
         self.lanes = None if lanes is None else max(1, int(lanes))
@@ -205,10 +206,8 @@ class SelfPlayScheduler:
         eng = self.engine
         per_rank = n_games // self.world + (1 if self.rank < n_games % self.world else 0)
 
-        def on_moves(m):
-            g = D.gather_moves(m, self.W * self.H, self.A) if D.is_distributed() else m
-            if g is None:
-                return
+        def on_moves(g):
+            # rank 0 (the replay owner): a batch of Move rows gathered from every rank (MoveExchange)
             if update and self.trainer is not None:
                 self.trainer.memory.add_moves(g)  # device replay ring: no per-record host objects
             elif update:
@@ -221,13 +220,12 @@ class SelfPlayScheduler:
                 self.result_queue.put({"reward": int(z), "swap_sides": bool(gid % 2)})
 
         def on_ply(_):
-            D.all_reduce_stats(eng.stats_vector())
             if update and self.trainer is not None:
                 self.trainer.pull(self.memory_queue)
                 for _ in range(self.updates_per_ply):
                     self.trainer.step()
 
-        eng.play_games(per_rank, on_moves=on_moves, on_ply=on_ply)
+        eng.play_games(per_rank, on_moves=on_moves, on_ply=on_ply, every=self.exchange_every)
         eng.check()
 
     def train_model(self, num_epochs=10, resume_model=False, resume_memory=False, num_workers=None,

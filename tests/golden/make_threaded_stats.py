@@ -203,6 +203,16 @@ def run_sequential(samples, procs=8):
     return out
 
 
+def _rounded(data):
+    """tree_probs / q to 8 decimals (float32 values: exact to their precision) for a compact file."""
+    for v in data.values():
+        for pos in v["positions"]:
+            for smp in pos["samples"]:
+                smp["tree_probs"] = [round(x, 8) for x in smp["tree_probs"]]
+                smp["q"] = round(smp["q"], 8)
+    return data
+
+
 def main():
     torch.multiprocessing.set_start_method("spawn")  # as the reference's entry points (main.py:109)
     os.chdir("/tmp")  # reference modules may write logs into cwd
@@ -220,18 +230,18 @@ def main():
             data["table_" + name] = dict(common, threads_per_worker=gt, net="table", salt=TABLE_SALT,
                                          positions=run_threaded(TableNetModule(7, TABLE_SALT), 400,
                                                                 "table_" + name, gt))
-            json.dump(data, open(OUT, "w"))
+            json.dump(_rounded(data), open(OUT, "w"), separators=(",", ":"))
         if which in ("resnet", "resnet_" + name, "all"):
             torch.set_num_threads(6)
             net, sums = _resnet()
             data["resnet_" + name] = dict(common, threads_per_worker=gt, net=rn, net_checksums=sums,
                                           positions=run_threaded(net, 160, "resnet_" + name, gt))
-            json.dump(data, open(OUT, "w"))
+            json.dump(_rounded(data), open(OUT, "w"), separators=(",", ":"))
     if which in ("resnet_seq", "all"):
         _, sums = _resnet()
         data["resnet_seq"] = dict(common, thread_count=1, threads_per_worker=1, net=rn, net_checksums=sums,
                                   positions=run_sequential(160))
-        json.dump(data, open(OUT, "w"))
+        json.dump(_rounded(data), open(OUT, "w"), separators=(",", ":"))
     print("done")
 
 

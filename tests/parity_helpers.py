@@ -118,7 +118,7 @@ def _eval_table(arena, salts_by_tree, n):
     return probs, values
 
 
-def run_g2_group(cases, leaf_format="f32", leaf_layout="nchw", search_threads=1, tapes=None):
+def run_g2_group(cases, leaf_format="f32", leaf_layout="nchw", search_threads=1, tapes=None, blocks_per_tree=0):
     """Run a group of G2 cases (same game / sims / strong_play) as trees of one arena.
 
     search_threads=K > 1: the threaded (virtual-loss) search, ceil(sims / K) select steps;
@@ -130,7 +130,7 @@ def run_g2_group(cases, leaf_format="f32", leaf_layout="nchw", search_threads=1,
     game, sims, strong = cases[0]["game"], cases[0]["sims"], cases[0]["strong_play"]
     n = len(cases)
     arena = Arena(game, n_trees=n, iterations=sims, rng="tape", strong_play=strong, leaf_format=leaf_format,
-                  leaf_layout=leaf_layout, search_threads=search_threads)
+                  leaf_layout=leaf_layout, search_threads=search_threads, blocks_per_tree=blocks_per_tree)
     arena.set_tapes(tapes if tapes is not None else [g2_tape(c) for c in cases])
     salts_by_tree = torch.tensor([c["salt"] for c in cases], dtype=torch.int64, device=arena.device)
 
@@ -162,7 +162,7 @@ def run_g2_group(cases, leaf_format="f32", leaf_layout="nchw", search_threads=1,
     return res, counters
 
 
-def run_g3_group(games, leaf_format="f32", leaf_layout="nchw", search_threads=1):
+def run_g3_group(games, leaf_format="f32", leaf_layout="nchw", search_threads=1, blocks_per_tree=0):
     """Run a group of G3 games (same game / sims / evaluate) as game slots of one arena (tape mode).
 
     search_threads=K > 1: threaded search, tapes from the oracle's threaded replay."""
@@ -173,7 +173,8 @@ def run_g3_group(games, leaf_format="f32", leaf_layout="nchw", search_threads=1)
     game, sims, evaluate = games[0]["game"], games[0]["sims"], games[0]["evaluate"]
     G = len(games)
     arena = Arena(game, n_trees=2 * G, n_games=G, iterations=sims, rng="tape", evaluate=evaluate,
-                  leaf_format=leaf_format, leaf_layout=leaf_layout, search_threads=search_threads)
+                  leaf_format=leaf_format, leaf_layout=leaf_layout, search_threads=search_threads,
+                  blocks_per_tree=blocks_per_tree)
     tapes = []
     for g in games:
         tp, to, _ = g3_tapes(g, search_threads)

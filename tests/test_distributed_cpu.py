@@ -1,5 +1,7 @@
-"""CPU: the multi-GPU exchange steps (episode-stat all_reduce, Move gather to rank 0,
-weight broadcast) with torch.distributed gloo, world size 2."""
+"""CPU: the multi-GPU exchange steps with torch.distributed gloo, world sizes 2 and 4: the
+episode-batch MoveExchange (Move rows staged per rank, one header all_gather + one gather to rank 0
+per round, statistics summed in the same round), the engines' play_games loops that end on it,
+and the primitives (stats all_reduce, Move gather, max, weight broadcast)."""
 import os
 import tempfile
 
@@ -62,18 +64,29 @@ class _FakeArena:
 
 class _FakeEngine:
     """Stands in for SelfPlayEngine inside its own play_games loop: rank r finishes r + 1 games per
-    ply, and every ply runs the same per-ply collectives as the scheduler (gather + stats)."""
+    ply (while it has games left) and exports one Move record per finished game."""
 
-    def __init__(self, rate):
+    def __init__(self, rate, rank=0):
         self.arena = _FakeArena(4)
         self.games_done = 0
         self.rate = rate
+        self.rank = rank
         self.plies_run = 0
+        self._limit = 0
 
     def ply(self, on_moves=None):
         self.plies_run += 1
-        self.games_done += self.rate
-        on_moves(_moves(0, 0))
+        k = max(0, min(self.rate, self._limit - self.games_done))
+        m = _moves(self.rank, k)
+        m["game"] = torch.arange(self.games_done, self.games_done + k, dtype=torch.int64) + 1000 * self.rank
+        self.games_done += k
+        on_moves(m)
+
+    def stats_vector(self):
+        return [self.games_done, 0, 0, 0, 0, 0, 0, 0]
+
+    def _record_shape(self):
+        return 42, 7
 
     def _play_games_setup(self, n):
         from self_play_reinforcement_learning_amd.engine import SelfPlayEngine
@@ -87,31 +100,38 @@ def _loop_worker(rank, world, port, q):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       SPMCTS_DIST_INIT="file://" + port)
     D.init_from_env(backend="gloo")
-    eng = _FakeEngine(rate=rank + 1)
+    eng = _FakeEngine(rate=rank + 1, rank=rank)
     gathered = []
-    plies = SelfPlayEngine.play_games(
-        eng, 6, on_moves=lambda m: gathered.append(D.gather_moves(m, 42, 7)),
-        on_ply=lambda e: D.all_reduce_stats([e.games_done]))
-    q.put((rank, plies, eng.games_done, len(gathered)))
+    plies = SelfPlayEngine.play_games(eng, 6, on_moves=lambda m: gathered.append(m["game"].tolist()), every=4)
+    q.put((rank, plies, eng.games_done, gathered))
     torch.distributed.destroy_process_group()
 
 
-def test_play_games_keeps_ranks_in_step_gloo():
-    """Ranks that finish their share early keep stepping until every rank is done, so the
-    per-ply collectives (Move gather, stats all_reduce) always match (no deadlock)."""
+@pytest.mark.parametrize("world", [2, 4])
+def test_play_games_keeps_ranks_in_step_gloo(world):
+    """Ranks that finish their share early keep stepping idle plies until an exchange round finds
+    every rank done (so the rounds always match, no deadlock); every finished game's records reach
+    rank 0 exactly once, batched per round (every 4 plies), and no other rank's sink is called."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_loop_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_loop_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=120) for _ in procs], key=lambda x: x[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (r0, p0, d0, g0), (r1, p1, d1, g1) = res
-    assert p0 == p1 == 6 and g0 == g1 == 6  # rank 0 needs 6 plies for its 6 games; rank 1 idles along
-    assert d0 == 6 and d1 == 12
+    # rank 0 (1 game per ply) needs 6 plies -> the round after ply 8 finds everyone done
+    assert all(r[1] == 8 for r in res)
+    assert all(r[2] == 6 for r in res)
+    assert all(r[3] == [] for r in res[1:])
+    rounds = res[0][3]
+    assert len(rounds) == 2
+    got = sorted(g for batch in rounds for g in batch)
+    assert got == sorted(1000 * r + i for r in range(world) for i in range(6))
+    # a round holds rank 0's rows first, then rank 1's, ...
+    assert rounds[0][:4] == [0, 1, 2, 3] and rounds[0][4] == 1000
 
 
 class _FakeLane(_FakeEngine):
@@ -134,11 +154,12 @@ class _FakeLane(_FakeEngine):
 
     def _ply_finish(self, on_moves=None, refill=True, game_offset=0):
         self.plies_run += 1
-        self.games_done += self.rate
-        m = _moves(0, 1)
-        m["game"] += game_offset
+        k = max(0, min(self.rate, self._limit - self.games_done))
+        m = _moves(self.rank, k)
+        m["game"] = torch.arange(self.games_done, self.games_done + k, dtype=torch.int64) + 1000 * self.rank + game_offset
+        self.games_done += k
         on_moves(m)
-        return self.rate, 1
+        return k, k
 
 
 def _laned_worker(rank, world, port, q):
@@ -148,25 +169,20 @@ def _laned_worker(rank, world, port, q):
                       SPMCTS_DIST_INIT="file://" + port)
     D.init_from_env(backend="gloo")
     eng = LanedEngine.__new__(LanedEngine)  # lanes without a GPU: no streams, fake arenas
-    eng.lanes = [_FakeLane(rate=rank + 1), _FakeLane(rate=1)]
+    eng.lanes = [_FakeLane(rate=rank + 1, rank=rank), _FakeLane(rate=1, rank=rank)]
     eng.streams = [None, None]
     eng.iterations = 3
     eng.select_steps = 3
     eng.device = torch.device("cpu")
     games = []
-
-    def on_moves(m):
-        games.append(int(m["game"][0]))
-        D.gather_moves(m, 42, 7)
-
-    plies = eng.play_games(8, on_moves=on_moves, on_ply=lambda e: D.all_reduce_stats([e.games_done]))
-    q.put((rank, plies, [ln.games_done for ln in eng.lanes], games[:2]))
+    plies = eng.play_games(8, on_moves=lambda m: games.extend(m["game"].tolist()), every=2)
+    q.put((rank, plies, [ln.games_done for ln in eng.lanes], games))
     torch.distributed.destroy_process_group()
 
 
 def test_laned_engine_play_games_gloo():
-    """LanedEngine splits the games over its lanes, every lane steps every ply (so the per-lane
-    collectives in on_moves match across ranks), and lane i's game ids carry the i * 2**40 offset."""
+    """LanedEngine splits the games over its lanes, every lane steps every ply, both lanes' records
+    go through one exchange, and lane i's game ids carry the i * 2**40 offset."""
     from self_play_reinforcement_learning_amd.engine import LanedEngine
 
     ctx = mp.get_context("spawn")
@@ -180,10 +196,13 @@ def test_laned_engine_play_games_gloo():
         p.join(timeout=60)
         assert p.exitcode == 0
     (_, p0, d0, g0), (_, p1, d1, g1) = res
-    # 8 games = 4 per lane; the slowest lane (rate 1) needs 4 plies on both ranks
+    # 8 games = 4 per lane; the slowest lane (rate 1) needs 4 plies, a round every 2 plies
     assert p0 == p1 == 4
-    assert d0 == [4, 4] and d1 == [8, 4]
-    assert g0 == [0, LanedEngine.GAME_ID_STRIDE] and g1 == g0
+    assert d0 == [4, 4] and d1 == [4, 4]
+    assert g1 == []
+    S = LanedEngine.GAME_ID_STRIDE
+    assert sorted(g0) == sorted([i for i in range(4)] + [S + i for i in range(4)] +
+                                [1000 + i for i in range(4)] + [S + 1000 + i for i in range(4)])
 
 
 def test_pack_unpack_roundtrip():
@@ -193,22 +212,78 @@ def test_pack_unpack_roundtrip():
         assert torch.equal(back[k].reshape(m[k].shape), m[k]), k
 
 
-def test_two_rank_exchange_gloo():
+@pytest.mark.parametrize("world", [2, 4])
+def test_exchange_primitives_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=120) for _ in procs], key=lambda x: x[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (r0, s0, g0, mx0, w0), (r1, s1, g1, mx1, w1) = res
-    assert s0 == s1 == [3, 10, 2, 0, 0, 0, 2, 0]
-    assert mx0 == mx1 == 1.5
-    assert w0 == w1 == 0.0  # rank 0's weights everywhere
-    assert g1 is None
-    exp = {k: torch.cat([_moves(0, 3)[k], _moves(1, 5)[k]]) for k in g0}
+    want = [sum(r + 1 for r in range(world)), sum(10 * r for r in range(world)), world, 0, 0, 0, world, 0]
+    assert all(r[1] == want for r in res)
+    assert all(r[3] == 1.5 * (world - 1) for r in res)
+    assert all(r[4] == 0.0 for r in res)  # rank 0's weights everywhere
+    assert all(r[2] is None for r in res[1:])
+    g0 = res[0][2]
+    exp = {k: torch.cat([_moves(r, 3 + 2 * r)[k] for r in range(world)]) for k in g0}
     for k in exp:
         assert torch.equal(g0[k].reshape(exp[k].shape), exp[k]), k
+
+
+def _exchange_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      SPMCTS_DIST_INIT="file://" + port)
+    D.init_from_env(backend="gloo")
+    got = []
+    ex = D.MoveExchange(42, 7, sink=lambda m: got.append({k: v.clone() for k, v in m.items()}), every=3)
+    out = []
+    for ply in range(7):
+        ex.stage(_moves(10 * rank + ply, (rank + ply) % 3))  # 0..2 records per ply, some plies none
+        out.append(ex.end_ply(lambda: [rank, ply], done=ply >= 2 + rank))
+    out.append(ex.end_ply(lambda: [rank, 99], done=True, force=True))
+    q.put((rank, out, got, ex.rounds))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_move_exchange_rounds_gloo(world):
+    """Rounds every 3 plies (+ one forced): None between rounds; at a round every rank sees the
+    same (all-done, summed stats); rank 0 receives exactly the rows staged since the previous round,
+    rank by rank, bit-exact after the device pack/unpack; the other ranks' sinks are never called."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in procs], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, out, got, rounds in res:
+        assert rounds == 3
+        assert [o is None for o in out] == [True, True, False, True, True, False, True, False]
+    for i in (2, 5, 7):
+        assert len({str(r[1][i]) for r in res}) == 1  # identical on every rank
+    ply2, ply5, last = res[0][1][2], res[0][1][5], res[0][1][7]
+    assert ply2 == (world == 1, [sum(range(world)), 2 * world])
+    assert ply5[0] == (5 >= 2 + world - 1) and ply5[1] == [sum(range(world)), 5 * world]
+    assert last == (True, [sum(range(world)), 99 * world])
+    assert all(r[2] == [] for r in res[1:])
+    got = res[0][2]
+    batches = [(0, 3), (3, 6), (6, 7)]
+    nonempty = []
+    for lo, hi in batches:
+        parts = [_moves(10 * r + p, (r + p) % 3) for r in range(world) for p in range(lo, hi)]
+        parts = [m for m in parts if m["z"].shape[0]]
+        if parts:
+            nonempty.append({k: torch.cat([m[k] for m in parts]) for k in parts[0]})
+    assert len(got) == len(nonempty)
+    for g, e in zip(got, nonempty):
+        for k in e:
+            assert torch.equal(g[k].reshape(e[k].shape), e[k]), k

@@ -85,6 +85,21 @@ def _g2_groups():
 def test_search_matches_reference(key):
     cases = dict(_g2_groups())[key]
     res, counters = run_g2_group(cases)
+    _check_g2(cases, res, counters)
+
+
+@pytest.mark.parametrize("key", [k for k, _ in _g2_groups()], ids=lambda k: f"{k[0]}-{k[1]}-strong{int(k[2])}")
+def test_search_matches_reference_with_subtree_recycling(key):
+    """The node store below the worst case (blocks_per_tree = one search + 4): every search begins
+    with a compaction of the tree (k_compact: the opening's dead blocks dropped, the root moved to
+    block 0, live blocks slid down); results stay bit-exact."""
+    cases = dict(_g2_groups())[key]
+    res, counters = run_g2_group(cases, blocks_per_tree=key[1] + 1 + 2 + 4)
+    assert counters["compactions"] == sum(1 for c in cases if len(c["opening"]) >= 2)
+    _check_g2(cases, res, counters)
+
+
+def _check_g2(cases, res, counters):
     assert counters["error_flags"] == 0
     for c, r in zip(cases, res):
         assert r["root_player"] == c["root_player"], c["id"]
@@ -116,6 +131,23 @@ def _g3_groups():
 def test_selfplay_games_match_reference(key):
     games = dict(_g3_groups())[key]
     moves, counters = run_g3_group(games)
+    _check_g3(games, moves, counters)
+
+
+@pytest.mark.parametrize("key", [k for k, _ in _g3_groups()], ids=lambda k: f"{k[0]}-{k[1]}-eval{int(k[2])}")
+def test_selfplay_games_match_reference_with_subtree_recycling(key):
+    """Whole games with a node store of 6 searches' worth of blocks: trees are compacted many times
+    per game (subtrees above the active root recycled); Moves and results stay bit-exact and the
+    high-water mark stays within the store."""
+    games = dict(_g3_groups())[key]
+    cap = 6 * key[1] + 64
+    moves, counters = run_g3_group(games, blocks_per_tree=cap)
+    assert counters["compactions"] > 0
+    assert counters["blocks_in_use_max"] <= cap
+    _check_g3(games, moves, counters)
+
+
+def _check_g3(games, moves, counters):
     assert counters["error_flags"] == 0
     assert counters["games_finished"] == len(games)
     # results breakdown [swap][win, draw, loss] from the policy's perspective
@@ -241,14 +273,17 @@ def test_threaded_search_matches_oracle(key, threads):
 @pytest.mark.gpu
 @pytest.mark.parametrize("threads", [3, 4])
 @pytest.mark.parametrize("key", [k for k, _ in _g3_groups()])
-def test_threaded_selfplay_games_match_oracle(key, threads):
+@pytest.mark.parametrize("recycle", [False, True], ids=["full-store", "recycled"])
+def test_threaded_selfplay_games_match_oracle(key, threads, recycle):
     """Whole self-play games in games mode with K sims in flight per tree (set_node expansions in
-    slot 0 of the tree, budget-bounded last step), bit-exact vs the oracle's threaded episodes."""
+    slot 0 of the tree, budget-bounded last step), bit-exact vs the oracle's threaded episodes —
+    also with a node store of 6 searches' worth of blocks (subtree recycling, k_compact)."""
     from tests.parity_helpers import g3_tapes
 
     games = dict(_g3_groups())[key]
-    moves, counters = run_g3_group(games, search_threads=threads)
+    moves, counters = run_g3_group(games, search_threads=threads, blocks_per_tree=6 * key[1] + 64 if recycle else 0)
     assert counters["error_flags"] == 0
+    assert (counters["compactions"] > 0) == recycle
     assert counters["games_finished"] == len(games)
     exp_results = np.zeros((2, 3), dtype=np.int64)
     by_game = {}

@@ -145,3 +145,148 @@ def test_philox_visit_distribution_matches_reference_with_resnet():
     fc, fg = np.bincount(ca, minlength=7) / M, np.bincount(ga, minlength=7) / N
     sef = np.sqrt(fc * (1 - fc) / M + fg * (1 - fg) / N)
     assert (np.abs(fc - fg) <= 4.5 * sef + 2e-3).all(), (fc, fg)
+
+
+# ------------------------------------------------------------------ threaded search vs the reference (G6)
+# tests/golden/threaded_stats.json (tests/golden/make_threaded_stats.py) holds root visit distributions
+# of the REFERENCE's own threaded search: MCTreeSearch(thread_count=4) behind a real InferenceProxy /
+# InferenceWorker process (mcts.py:154, :328-367; inference_worker.py:89-119), 200 sims, Connect4, at
+# three positions, in two regimes: "single" = one game thread per worker (its 4 search threads only)
+# and "serving" = 8 game threads sharing the worker's queue pool (the reference's default
+# threads_per_worker).  In "serving" the reference's check-then-lock race (is_leaf before
+# lock.acquire, mcts.py:357-359) re-expands ~14 % of leaves (counts in the fixture), which flattens
+# its visit distributions; the arena implements the race-free rolling schedule.
+def _g6(name):
+    from tests.parity_helpers import load_json
+
+    return load_json("threaded_stats.json")[name]
+
+
+def _ref_samples(pos):
+    tp = np.array([s["tree_probs"] for s in pos["samples"]], dtype=np.float64)
+    act = np.array([s["action"] for s in pos["samples"]])
+    return tp, act
+
+
+def _gpu_threaded(opening, N, sims, K, net=None, salt=None):
+    """N Philox trees searched from `opening` with K sims in flight (the arena's rolling schedule)."""
+    from self_play_reinforcement_learning_amd.arena import Arena, table_net_eval
+    from tests.parity_helpers import empty_prior
+
+    if net is None:
+        arena = Arena("connect4", n_trees=N, iterations=sims, rng="philox", seed=321, leaf_format="f32",
+                      search_threads=K)
+
+        def ev(x):
+            return table_net_eval("connect4", x, "f32", "nchw", salt=salt)
+
+        arena.tree_reset(list(range(N)), [1] * N, priors=np.tile(empty_prior("connect4", salt), (N, 1)))
+    else:
+        arena = Arena("connect4", n_trees=N, iterations=sims, rng="philox", seed=321, leaf_format=net.leaf_format,
+                      leaf_layout=net.leaf_layout, search_threads=K)
+        ev = net
+        root_p, _ = net(net.empty_root_input(7, 6, arena.device))
+        arena.set_root_prior(root_p[0])
+        arena.tree_reset(list(range(N)), [1] * N)
+
+    def step(count):
+        if count:
+            p, v = ev(arena.leaves(count))
+            arena.expand(p, v)
+
+    for a in opening:
+        step(arena.play_action(list(range(N)), [a] * N))
+    arena.search_begin(list(range(N)))
+    for _ in range(-(-sims // K)):
+        step(arena.select())
+    out = arena.search_end(1.0)
+    c = arena.counters()
+    arena.check()
+    res = out["tree_probs"].double().cpu().numpy(), out["action"].cpu().numpy(), c
+    arena.close()
+    return res
+
+
+def _close(cp, gp, ca, ga):
+    """The stated tolerance: every mean visit fraction and chosen-action frequency within 4.5 standard
+    errors of the difference (per-sample variances of both sides) + 2e-3."""
+    M, N = len(cp), len(gp)
+    se = np.sqrt(cp.var(0, ddof=1) / M + gp.var(0, ddof=1) / N)
+    ok_p = (np.abs(cp.mean(0) - gp.mean(0)) <= 4.5 * se + 2e-3).all()
+    fc, fg = np.bincount(ca, minlength=7) / M, np.bincount(ga, minlength=7) / N
+    sef = np.sqrt(fc * (1 - fc) / M + fg * (1 - fg) / N)
+    ok_a = (np.abs(fc - fg) <= 4.5 * sef + 2e-3).all()
+    return ok_p and ok_a, (cp.mean(0).round(4), gp.mean(0).round(4), se.round(4))
+
+
+def _resnet_evaluator(d):
+    from self_play_reinforcement_learning_amd.evaluator import HipTowerEvaluator
+    from self_play_reinforcement_learning_amd.modules import ResidualTower
+
+    torch.manual_seed(0)
+    net = ResidualTower(7, 6, 7, num_blocks=20, filter_factor=32).eval()
+    sums = {k: float(v.double().sum()) for k, v in net.state_dict().items()}
+    for k, v in d["net_checksums"].items():  # the reference's net, bit for bit at init
+        assert abs(sums[k] - v) <= 1e-6 * max(1.0, abs(v)), k
+    return HipTowerEvaluator(net.cuda())
+
+
+@pytest.mark.parametrize("pi", [0, 1, 2])
+def test_threaded_search_matches_reference_table(pi):
+    d = _g6("table_single")
+    pos = d["positions"][pi]
+    cp, ca = _ref_samples(pos)
+    gp, ga, c = _gpu_threaded(pos["opening"], 4096, d["sims"], d["thread_count"], salt=d["salt"])
+    assert c["sims"] + c["leaked_sims"] == d["sims"] * 4096
+    ok, info = _close(cp, gp, ca, ga)
+    assert ok, info
+
+
+@pytest.mark.parametrize("pi", [0, 1, 2])
+def test_threaded_search_matches_reference_resnet(pi):
+    """The headline configuration: ResNet-128x20 (the reference's seed-0 init, checked), 200 sims,
+    4 sims in flight, through the fused bf16 HIP tower (bf16 perturbs priors by ~1e-3)."""
+    d = _g6("resnet_single")
+    pos = d["positions"][pi]
+    cp, ca = _ref_samples(pos)
+    gp, ga, _ = _gpu_threaded(pos["opening"], 2048, d["sims"], d["thread_count"], net=_resnet_evaluator(d))
+    ok, info = _close(cp, gp, ca, ga)
+    assert ok, info
+
+
+@pytest.mark.parametrize("pi", [0, 1, 2])
+def test_sequential_search_matches_reference_resnet(pi):
+    """K = 1 at the headline net and budget: the reference's sequential mode (direct network)."""
+    d = _g6("resnet_seq")
+    pos = d["positions"][pi]
+    cp, ca = _ref_samples(pos)
+    gp, ga, _ = _gpu_threaded(pos["opening"], 2048, d["sims"], 1, net=_resnet_evaluator(d))
+    ok, info = _close(cp, gp, ca, ga)
+    assert ok, info
+
+
+def test_threaded_statistical_check_has_power():
+    """Negative control: the sequential (K = 1) search is rejected against the reference's threaded
+    samples by the same tolerance."""
+    d = _g6("table_single")
+    pos = d["positions"][2]
+    cp, ca = _ref_samples(pos)
+    gp, ga, _ = _gpu_threaded(pos["opening"], 4096, d["sims"], 1, salt=d["salt"])
+    assert not _close(cp, gp, ca, ga)[0]
+
+
+@pytest.mark.parametrize("pi", [0, 1, 2])
+def test_threaded_search_vs_reference_serving_regime(pi):
+    """The reference's default deployment (8 game threads per worker) races (G6 re-expansion counts);
+    the arena's race-free search must sit where the reference's own race-light run sits: its distance
+    to the serving-regime samples is at most the reference's single-vs-serving distance + tolerance."""
+    d_s, d_v = _g6("table_single"), _g6("table_serving")
+    assert d_v["positions"][pi]["re_expansions"] > 4 * d_s["positions"][pi]["re_expansions"]
+    sp, _ = _ref_samples(d_s["positions"][pi])
+    vp, _ = _ref_samples(d_v["positions"][pi])
+    gp, _, _ = _gpu_threaded(d_v["positions"][pi]["opening"], 4096, d_v["sims"], d_v["thread_count"],
+                             salt=d_v["salt"])
+    se = np.sqrt(vp.var(0, ddof=1) / len(vp) + gp.var(0, ddof=1) / len(gp) + sp.var(0, ddof=1) / len(sp))
+    gap_ref = np.abs(sp.mean(0) - vp.mean(0))
+    gap_gpu = np.abs(gp.mean(0) - vp.mean(0))
+    assert (gap_gpu <= gap_ref + 4.5 * se + 2e-3).all(), (gap_ref.round(4), gap_gpu.round(4))
