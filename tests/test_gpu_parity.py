@@ -95,7 +95,8 @@ def test_search_matches_reference_with_subtree_recycling(key):
     block 0, live blocks slid down); results stay bit-exact."""
     cases = dict(_g2_groups())[key]
     res, counters = run_g2_group(cases, blocks_per_tree=key[1] + 1 + 2 + 4)
-    assert counters["compactions"] == sum(1 for c in cases if len(c["opening"]) >= 2)
+    # used = 2 + one block per opening move; a search needs sims + K + 2 blocks free -> openings of >= 3
+    assert counters["compactions"] == sum(1 for c in cases if len(c["opening"]) >= 3)
     _check_g2(cases, res, counters)
 
 
@@ -136,15 +137,20 @@ def test_selfplay_games_match_reference(key):
 
 @pytest.mark.parametrize("key", [k for k, _ in _g3_groups()], ids=lambda k: f"{k[0]}-{k[1]}-eval{int(k[2])}")
 def test_selfplay_games_match_reference_with_subtree_recycling(key):
-    """Whole games with a node store of 6 searches' worth of blocks: trees are compacted many times
+    """Whole games with a node store of 3-6 searches' worth of blocks: trees are compacted many times
     per game (subtrees above the active root recycled); Moves and results stay bit-exact and the
     high-water mark stays within the store."""
     games = dict(_g3_groups())[key]
-    cap = 6 * key[1] + 64
+    cap = _recycle_cap(key[0], key[1])
     moves, counters = run_g3_group(games, blocks_per_tree=cap)
     assert counters["compactions"] > 0
     assert counters["blocks_in_use_max"] <= cap
     _check_g3(games, moves, counters)
+
+
+def _recycle_cap(game, sims):
+    """A node store well below the worst case (2 + ceil(cells/2) * sims + cells + 2 blocks)."""
+    return 6 * sims + 64 if game == "connect4" else 3 * sims + 16
 
 
 def _check_g3(games, moves, counters):
@@ -281,7 +287,7 @@ def test_threaded_selfplay_games_match_oracle(key, threads, recycle):
     from tests.parity_helpers import g3_tapes
 
     games = dict(_g3_groups())[key]
-    moves, counters = run_g3_group(games, search_threads=threads, blocks_per_tree=6 * key[1] + 64 if recycle else 0)
+    moves, counters = run_g3_group(games, search_threads=threads, blocks_per_tree=_recycle_cap(key[0], key[1]) if recycle else 0)
     assert counters["error_flags"] == 0
     assert (counters["compactions"] > 0) == recycle
     assert counters["games_finished"] == len(games)
