@@ -36,6 +36,7 @@ sys.path.insert(0, HERE)
 
 TRAFFIC_FILE = os.path.join(HERE, "profiles", "r01_bench_prof", "k_tower_traffic.json")  # --search-threads 1
 TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r01_bench_prof_k4", "k_tower_traffic.json")  # 4 (default)
+TREE_TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r02_tree_pmc", "tree_traffic.json")
 
 # MI355X reference figures (/opt/skills/guides/MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
@@ -70,6 +71,19 @@ def select_bytes(sims, levels, A=7, threads=1):
     per_level = 20 * A + 4 + 16 if threads <= 1 else 24 * A + 4 + 4 + 4
     per_sim = 90 + 8 * A + 128 + 38 + (4 if threads > 1 else 0)
     return levels * per_level + sims * per_sim
+
+
+def expand_bytes(nn_leaves, path_nodes, A=7, threads=1):
+    """Algorithmic HBM bytes of the backups in k_expand / k_expand_vl (block init +
+    path read-modify-write), per network leaf: its outputs (4A + 4), the new child block (A x {n i32,
+    w f64, p f32, child i32, dtype u8, vl i32} = 25A, + valid mask 4), the leaf's own n/w RMW and
+    child index (28), the slot record (node ids, boards, mover, row: 30) and the tree's block
+    counter + counters (24); per path node n, w and vl read-modify-write + its id (36 with virtual
+    loss, 28 without: n/w only).  The refill selects the rolling schedule runs inside k_expand_vl are
+    counted by select_bytes."""
+    per_leaf = 4 * A + 4 + 25 * A + 4 + 28 + 30 + 24
+    per_path = 36 if threads > 1 else 28
+    return nn_leaves * per_leaf + path_nodes * per_path
 
 
 def _cpu_worker(args):
@@ -143,6 +157,8 @@ def main():
     ap.add_argument("--mode", choices=["selfplay", "arena"], default="selfplay")
     ap.add_argument("--lanes", type=int, default=2,
                     help="arenas per GPU on their own HIP streams (engine.LanedEngine); 1 = one arena")
+    ap.add_argument("--blocks-per-tree", type=int, default=0,
+                    help="node blocks per tree; below the worst case the arena recycles subtrees (k_compact)")
     ap.add_argument("--no-pack", action="store_true",
                     help="lanes > 1: keep round-aligned tower tiles (no SPMCTS_TOWER_PACK)")
     ap.add_argument("--search-threads", type=int, default=4,
@@ -177,7 +193,8 @@ def main():
         torch.manual_seed(1)
         opponent = ResidualTower(7, 6, 7, num_blocks=args.blocks, filter_factor=args.filter_factor).to(dev).eval()
     kw = dict(iterations=args.sims, seed=1234 + rank, device=dev, bucket=args.bucket, opponent=opponent,
-              evaluate=arena_mode, record=not arena_mode, search_threads=args.search_threads)
+              evaluate=arena_mode, record=not arena_mode, search_threads=args.search_threads,
+              blocks_per_tree=args.blocks_per_tree)
     if args.lanes > 1:
         eng = LanedEngine("connect4", net, n_games=args.games, lanes=args.lanes, pack=not args.no_pack, **kw)
     else:
@@ -221,15 +238,32 @@ def main():
     tot = D.all_reduce_stats([moves_local, c1["sims"] - c0["sims"], c1["games_finished"] - c0["games_finished"]])
     moves_all, sims_all, games_all = (int(x) for x in tot)
 
-    # ---- select-kernel roofline (HIP events around k_select on the arena's stream)
+    # ---- tree kernels (HIP events around k_select* / k_expand* on each lane's stream).  With K > 1
+    # the rolling schedule runs most selects inside k_expand_vl (each slot refilled right after its
+    # backup), so the two kernels are reported together: algorithmic bytes of every select level and
+    # every backup / block init over their summed durations.  With two lanes a tree kernel of one lane
+    # shares the chip with the other lane's tower dispatch, so these durations include that wait.
     sel_ms = eng.select_timer.total_ms()
+    exp_ms = eng.expand_timer.total_ms()
     sel_launches = eng.select_timer.count()
+    exp_launches = eng.expand_timer.count()
     sims_local = c1["sims"] - c0["sims"]
     levels_local = c1["depth_sum"] - c0["depth_sum"]
-    sel_bytes = select_bytes(sims_local, levels_local, threads=args.search_threads)
-    sel_avg_s = sel_ms / 1e3 / max(1, sel_launches)
-    bytes_per_launch = sel_bytes / max(1, sel_launches)
-    achieved = bytes_per_launch / sel_avg_s / 1e9 if sel_avg_s > 0 else 0.0
+    nn_local = c1["nn_leaves"] - c0["nn_leaves"]
+    path_nodes = levels_local * (nn_local / max(1, sims_local))
+    tree_bytes = select_bytes(sims_local, levels_local, threads=args.search_threads) + \
+        expand_bytes(nn_local, path_nodes, threads=args.search_threads)
+    tree_dispatches = sel_launches + exp_launches
+    tree_s = (sel_ms + exp_ms) / 1e3
+    bytes_per_launch = tree_bytes / max(1, tree_dispatches)
+    sel_avg_s = tree_s / max(1, tree_dispatches)
+    achieved = tree_bytes / tree_s / 1e9 if tree_s > 0 else 0.0
+    tree_traffic, tree_traffic_src = None, None
+    tfile = TREE_TRAFFIC_FILE_K4 if args.search_threads > 1 else None
+    if tfile and os.path.exists(tfile) and (args.games, args.sims, args.filter_factor, args.blocks) == (4096, 200, 32, 20):
+        with open(tfile) as f:
+            tree_traffic = json.load(f)["bytes_per_dispatch"]
+        tree_traffic_src = os.path.relpath(tfile, HERE)
 
     # ---- network (MFMA) share: busy time = union of the network launches of all lanes
     nn_ms = union_ms(eng.nn_timer.intervals(ref))
@@ -308,17 +342,23 @@ def main():
             "dispatches": tw_dispatches,
         },
         "tree_roofline": {
-            "kernel": ("k_select<C4> (PUCT tree walk)" if args.search_threads <= 1 else
-                       f"k_select_vl<C4> (PUCT tree walk, {args.search_threads} sims in flight per tree)"),
+            "kernel": ("k_select<C4> + k_expand<C4> (PUCT tree walk, backup)" if args.search_threads <= 1 else
+                       f"k_select_vl<C4> + k_expand_vl<C4> (rolling search, {args.search_threads} sims in flight per "
+                       f"tree: walks, backups, refills)"),
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": tree_traffic,
+            "traffic_unit": "bytes/dispatch (L2<->fabric, PMC, both kernels)",
+            "traffic_source": tree_traffic_src,
             "bytes_per_launch": bytes_per_launch,
             "avg_launch_us": sel_avg_s * 1e6,
-            "launches": sel_launches,
+            "launches": tree_dispatches,
+            "select": {"dispatches": sel_launches, "ms": sel_ms},
+            "expand": {"dispatches": exp_launches, "ms": exp_ms},
+            "note": "durations co-scheduled with the other lane's tower dispatch" if args.lanes > 1 else None,
         },
         "nn": {
             "bound": "mfma",
@@ -337,6 +377,10 @@ def main():
             "terminal_leaf_frac": (c1["terminal_leaves"] - c0["terminal_leaves"]) / max(1, sims_local),
             "games_finished": games_all,
             "select_ms_share": sel_ms / 1e3 / elapsed if elapsed else None,
+            "expand_ms_share": exp_ms / 1e3 / elapsed if elapsed else None,
+            "leaked_sims": c1["leaked_sims"] - c0["leaked_sims"],
+            "blocks_in_use_max": c1["blocks_in_use_max"],
+            "compactions": c1["compactions"] - c0["compactions"],
         },
         "cpu_baseline": None,
     }

@@ -230,6 +230,10 @@ class Arena:
             timer.stop()
             call("spmcts_leaf_rows", self.h, ptr(self._leaves), ptr(self._count), _stream())
 
+    def leaf_rows_async(self):
+        """Gather the pending leaves into network rows (k_scan_need + k_encode) without a select."""
+        call("spmcts_leaf_rows", self.h, ptr(self._leaves), ptr(self._count), _stream())
+
     def games_end_ply_async(self):
         call("spmcts_games_end_ply", self.h, ptr(self._leaves), ptr(self._count), _stream())
 

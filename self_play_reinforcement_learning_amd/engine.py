@@ -136,6 +136,7 @@ class SelfPlayEngine:
         self.plies = 0
         self.started = False
         self.select_timer = None
+        self.expand_timer = None
         self.nn_timer = None
         self.async_device = True  # device-count evaluators run a whole ply without host syncs
         for ev in (self.evaluator, self.evaluator1):  # outputs sized for every row the arena can emit
@@ -162,6 +163,7 @@ class SelfPlayEngine:
 
     def enable_timers(self, on=True):
         self.select_timer = EventTimer() if on else None
+        self.expand_timer = EventTimer() if on else None
         self.nn_timer = EventTimer() if on else None
         self.tower_timer = EventTimer() if on else None
         for ev in (self.evaluator, self.evaluator1):
@@ -232,10 +234,14 @@ class SelfPlayEngine:
             p1, v1 = self.evaluator1.forward_dev(a.leaves_from(a.seg1, cap1), a.segment_count_dev(1), cap1)
         if self.nn_timer is not None:
             self.nn_timer.stop()
+        if self.expand_timer is not None:
+            self.expand_timer.start()
         if self.evaluator1 is None:
             a.expand(probs, values)
         else:
             a.expand2(probs, values, p1, v1)
+        if self.expand_timer is not None:
+            self.expand_timer.stop()
 
     # --- one ply in phases (LanedEngine interleaves the phases of several engines on their streams)
     def _ply_begin(self):
@@ -243,9 +249,15 @@ class SelfPlayEngine:
             self.start()
         self.arena.games_begin_ply()
 
-    def _ply_simulation(self):
-        """One lock-step simulation of every searching tree, without a host synchronisation."""
-        self.arena.select_async(self.select_timer)
+    def _ply_simulation(self, step=0):
+        """One simulation step of every searching tree, without a host synchronisation.  With K > 1
+        sims in flight only the first step launches the select kernel (it fills the K slots); later
+        steps' selects run inside the expand kernel, which refills each slot right after its backup
+        (the rolling schedule, csrc/spmcts.hip), so they only gather the pending leaves into rows."""
+        if step == 0 or self.search_threads == 1:
+            self.arena.select_async(self.select_timer)
+        else:
+            self.arena.leaf_rows_async()
         self._eval_expand_dev(cap=self.n_games * self.search_threads)
 
     def _ply_move(self):
@@ -258,8 +270,8 @@ class SelfPlayEngine:
         self._ply_begin()
         a = self.arena
         if self._device_count_ok():
-            for _ in range(self.select_steps):
-                self._ply_simulation()
+            for i in range(self.select_steps):
+                self._ply_simulation(i)
             self._ply_move()
         else:
             for _ in range(self.select_steps):
@@ -425,7 +437,7 @@ class LanedEngine:
         self.select_steps = self.lanes[0].select_steps
         self.search_threads = self.lanes[0].search_threads
         self.evaluator = self.lanes[0].evaluator
-        self.select_timer = self.nn_timer = self.tower_timer = None
+        self.select_timer = self.expand_timer = self.nn_timer = self.tower_timer = None
 
     def _each(self, fn):
         out = []
@@ -461,10 +473,11 @@ class LanedEngine:
         self._each(lambda e: e.enable_timers(on))
         if on:
             self.select_timer = _SumTimer([e.select_timer for e in self.lanes])
+            self.expand_timer = _SumTimer([e.expand_timer for e in self.lanes])
             self.nn_timer = _SumTimer([e.nn_timer for e in self.lanes])
             self.tower_timer = _SumTimer([e.tower_timer for e in self.lanes])
         else:
-            self.select_timer = self.nn_timer = self.tower_timer = None
+            self.select_timer = self.expand_timer = self.nn_timer = self.tower_timer = None
 
     def refresh_network(self):
         self._lanes_wait_caller()
@@ -480,8 +493,8 @@ class LanedEngine:
                     res.append(e.ply(on_moves, refill, game_offset=i * self.GAME_ID_STRIDE))
         else:
             self._each(lambda e: e._ply_begin())
-            for _ in range(self.select_steps):
-                self._each(lambda e: e._ply_simulation())
+            for i in range(self.select_steps):
+                self._each(lambda e: e._ply_simulation(i))
             self._each(lambda e: e._ply_move())
             res = []
             for i, (e, st) in enumerate(zip(self.lanes, self.streams)):

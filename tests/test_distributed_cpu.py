@@ -146,7 +146,7 @@ class _FakeLane(_FakeEngine):
     def _ply_begin(self):
         self.sims = 0
 
-    def _ply_simulation(self):
+    def _ply_simulation(self, step=0):
         self.sims += 1
 
     def _ply_move(self):

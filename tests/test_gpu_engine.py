@@ -324,41 +324,69 @@ def _gravity_ok(board):
     return bool((filled[:, 1:] <= filled[:, :-1]).all())
 
 
-def test_full_size_selfplay_properties():
-    """The bench workload at its full size (BASELINE configs[1]: Connect4, 200 sims/move, 4,096
-    games, ResNet-128x20 on the fused tower, two lanes with packed tiles), checked through
-    size-independent properties: exact simulation / move / leaf accounting, every exported Move a
-    legal gravity-consistent position with a normalised, legal-only visit distribution, consistent
-    per-game results, no device error flags."""
+def _full_size(G, sims, ff, blocks, plies, threads, lanes=2, blocks_per_tree=0, seed=11):
+    """Size-independent properties of a full-size self-play run: exact simulation / move / leaf
+    accounting, every exported Move a legal gravity-consistent position with a normalised,
+    legal-only visit distribution, consistent per-game results, no device error flags."""
     from self_play_reinforcement_learning_amd.engine import LanedEngine
     from self_play_reinforcement_learning_amd.modules import ResidualTower
 
     torch.manual_seed(0)
-    net = ResidualTower(7, 6, 7, num_blocks=20, filter_factor=32).cuda().eval()
-    G, sims, plies = 4096, 200, 12
-    eng = LanedEngine("connect4", net, n_games=G, lanes=2, iterations=sims, seed=11)
+    net = ResidualTower(7, 6, 7, num_blocks=blocks, filter_factor=ff).cuda().eval()
+    eng = LanedEngine("connect4", net, n_games=G, lanes=lanes, iterations=sims, seed=seed, search_threads=threads,
+                      blocks_per_tree=blocks_per_tree)
     got = []
     eng.run(plies=plies, on_moves=lambda m: got.append({k: v.cpu().numpy() for k, v in m.items()}))
     eng.check()
     c = eng.counters()
     assert c["error_flags"] == 0
-    assert c["sims"] == G * sims * plies  # every slot searches every ply (finished slots refill)
+    # every slot searches every ply (finished slots refill): `sims` search_node calls per search,
+    # each completed (network or terminal leaf) or leaked (threaded mode only, mcts.py:349-354)
+    assert c["sims"] + c["leaked_sims"] == G * sims * plies
+    assert threads > 1 or c["leaked_sims"] == 0
     assert c["moves"] == G * plies
-    # each simulation ends in exactly one network leaf or one terminal leaf; the end-of-ply
-    # _set_node expansions add network leaves of their own (none for a terminal child)
     sim_nn = c["sims"] - c["terminal_leaves"]
     assert sim_nn <= c["nn_leaves"] <= sim_nn + c["set_node_expansions"]
-    moves = {k: np.concatenate([g[k] for g in got]) for k in got[0]}
-    assert len(moves["z"]) == c["positions_exported"] > 0
-    assert c["games_finished"] == len(np.unique(moves["game"]))
-    assert set(np.unique(moves["z"]).tolist()) <= {-1.0, 0.0, 1.0}
-    np.testing.assert_allclose(moves["tree_probs"].sum(1), 1.0, atol=1e-5)
-    boards = moves["state"].reshape(-1, 7, 6).astype(int)
-    for b, p in zip(boards, moves["tree_probs"]):
-        assert _gravity_ok(b)
-        assert (p[b[:, 5] != 0] == 0).all()  # full columns get no visits
-        assert (b == 1).sum() in ((b == -1).sum(), (b == -1).sum() - 1)
-    for gid in np.unique(moves["game"]):
-        zs = moves["z"][moves["game"] == gid]
-        assert (zs == 0).all() or sorted(np.unique(zs).tolist()) == [-1.0, 1.0]
+    if got:
+        moves = {k: np.concatenate([g[k] for g in got]) for k in got[0]}
+        assert len(moves["z"]) == c["positions_exported"] > 0
+        assert c["games_finished"] == len(np.unique(moves["game"]))
+        assert set(np.unique(moves["z"]).tolist()) <= {-1.0, 0.0, 1.0}
+        np.testing.assert_allclose(moves["tree_probs"].sum(1), 1.0, atol=1e-5)
+        boards = moves["state"].reshape(-1, 7, 6).astype(int)
+        for b, p in zip(boards, moves["tree_probs"]):
+            assert _gravity_ok(b)
+            assert (p[b[:, 5] != 0] == 0).all()  # full columns get no visits
+            assert (b == 1).sum() in ((b == -1).sum(), (b == -1).sum() - 1)
+        for gid in np.unique(moves["game"]):
+            zs = moves["z"][moves["game"] == gid]
+            assert (zs == 0).all() or sorted(np.unique(zs).tolist()) == [-1.0, 1.0]
+    return c
 
+
+def test_full_size_selfplay_properties():
+    """BASELINE configs[1] at full size in the sequential search mode (K = 1): Connect4, 200 sims/move,
+    4,096 games, ResNet-128x20 on the fused tower, two lanes with packed tiles, 12 plies."""
+    _full_size(4096, 200, 32, 20, 12, threads=1)
+
+
+def test_full_size_headline_bench_config():
+    """The exact bench.py default: 4,096 games, 200 sims, ResNet-128x20, two lanes, 4 sims in flight
+    per tree (the rolling threaded search), 12 plies."""
+    c = _full_size(4096, 200, 32, 20, 12, threads=4)
+    assert c["positions_exported"] > 0
+    print(f"headline: blocks_in_use_max {c['blocks_in_use_max']} leaked_sims {c['leaked_sims']}")
+
+
+def test_full_size_config3_recycled_store():
+    """BASELINE configs[2] at full size: 16,384 games, 800 sims/move, ResNet-256x20, 4 sims in flight,
+    two lanes — with a node store of 1,800 blocks per tree instead of the worst case 16,846
+    (11.8 GB instead of 92 GB): subtrees above the active root are recycled (k_compact) and the
+    high-water mark stays within the store.  6 plies: every policy tree searches 3 times, the third
+    search after a compaction."""
+    cap = 1800
+    c = _full_size(16384, 800, 64, 20, 6, threads=4, blocks_per_tree=cap, seed=12)
+    assert c["compactions"] > 0
+    assert c["blocks_in_use_max"] <= cap
+    print(f"config3: blocks_in_use_max {c['blocks_in_use_max']} of {cap}, compactions {c['compactions']}, "
+          f"leaked_sims {c['leaked_sims']}")
