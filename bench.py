@@ -86,11 +86,33 @@ def expand_bytes(nn_leaves, path_nodes, A=7, threads=1):
     return nn_leaves * per_leaf + path_nodes * per_path
 
 
+def _random_opening(rng, max_len=16):
+    """A non-terminal Connect4 position after 0..max_len uniformly random legal moves (the worker's
+    next game starts there), so a short sample covers the mid-game positions a steady-state
+    self-play run searches, not only openings."""
+    from oracle.envs import Connect4Env
+
+    while True:
+        env, acts, player = Connect4Env(), [], 1
+        ok = True
+        for _ in range(rng.randint(0, max_len)):
+            legal = [a for a in range(7) if env.valid_moves()[a]]
+            a = legal[rng.randint(len(legal))]
+            _, _, done, _ = env.step(a, player)
+            if done:
+                ok = False
+                break
+            acts.append(a)
+            player = -player
+        if ok:
+            return acts
+
+
 def _cpu_worker(args):
-    """One host process: the oracle's sequential search (the reference's MCTreeSearch algorithm,
-    numpy RNG) + the reference-architecture ResNet in fp32 torch on ONE thread, Connect4 games
-    from the empty board, complete moves only, for `seconds`."""
-    seconds, seed, sims, filter_factor, num_blocks, threads = args
+    """One host process: the oracle's search (the reference's MCTreeSearch algorithm, numpy RNG) +
+    the reference-architecture ResNet in fp32 torch on ONE thread, complete moves only, for
+    `seconds`.  Games start at random mid-game positions (`openings`) or from the empty board."""
+    seconds, seed, sims, filter_factor, num_blocks, threads, openings = args
     import numpy as np
     import torch
 
@@ -102,9 +124,19 @@ def _cpu_worker(args):
     torch.manual_seed(0)
     net = ResidualTower(7, 6, 7, num_blocks=num_blocks, filter_factor=filter_factor).eval()
     np.random.seed(seed)
+    rng = np.random.RandomState(seed + 1)
     moves = 0
-    with torch.no_grad():
+
+    def new_game():
         tree, env, player = OracleTree("connect4", net, NumpyRNG(), sims, threads=threads), Connect4Env(), 1
+        for a in (_random_opening(rng) if openings else []):  # play_action flips the root's player
+            tree.play_action(a)
+            env.step(a, player)
+            player = -player
+        return tree, env, player
+
+    with torch.no_grad():
+        tree, env, player = new_game()
         t0 = time.time()
         while time.time() - t0 < seconds:
             a = tree.move()
@@ -113,30 +145,43 @@ def _cpu_worker(args):
             moves += 1
             player = -player
             if done:
-                env.reset()
-                tree, player = OracleTree("connect4", net, NumpyRNG(), sims, threads=threads), 1
+                tree, env, player = new_game()
         dt = time.time() - t0
     return moves, dt
 
 
-def cpu_baseline(seconds, cores, sims, filter_factor, num_blocks, threads=1):
+def cpu_baseline(seconds, cores, sims, filter_factor, num_blocks, threads=1, openings=True):
     """The reference's CPU self-play structure restated: `cores` independent play processes (the
     reference runs one SelfPlayWorker per core, self_play_parallel.py:95-171), each running the
-    oracle's sequential search with a 1-thread fp32 ResNet, for about `seconds`; positions/s summed
-    over processes.  (No IPC inference batching: the reference's proxy adds queue round trips.)
-    threads > 1: the oracle's threaded (virtual-loss) search, same per-leaf network calls."""
+    oracle's search with a 1-thread fp32 ResNet, for about `seconds`; positions/s summed over
+    processes.  (No IPC inference batching: the reference's proxy adds queue round trips.)
+    threads > 1: the oracle's threaded (virtual-loss, rolling) search, same per-leaf network calls.
+    openings: games start after 0..16 random moves (mid-game positions, where terminal leaves
+    occur), else from the empty board."""
     import multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     with ctx.Pool(cores) as pool:
-        res = pool.map(_cpu_worker, [(seconds, 1000 + i, sims, filter_factor, num_blocks, threads) for i in range(cores)])
+        res = pool.map(_cpu_worker, [(seconds, 1000 + i, sims, filter_factor, num_blocks, threads, openings)
+                                     for i in range(cores)])
     moves = sum(m for m, _ in res)
     rate = sum(m / dt for m, dt in res)
-    return dict(value=rate, unit="positions/s", cores=cores, kind="port",
-                sample=f"{cores} processes x (oracle MCTS, {sims} sims/move, "
-                       f"{'sequential' if threads <= 1 else f'{threads} sims in flight (virtual loss)'}, numpy RNG + ResNet-"
-                       f"{4 * filter_factor}x{num_blocks} fp32 torch, 1 thread), Connect4 games from the empty board, "
-                       f"{moves} complete moves in ~{seconds:.0f} s")
+    out = dict(value=rate, unit="positions/s", cores=cores, kind="port",
+               sample=f"{cores} processes x (oracle MCTS, {sims} sims/move, "
+                      f"{'sequential' if threads <= 1 else f'{threads} sims in flight (virtual loss)'}, numpy RNG + ResNet-"
+                      f"{4 * filter_factor}x{num_blocks} fp32 torch, 1 thread), Connect4 games "
+                      f"{'from random 0-16-move openings' if openings else 'from the empty board'}, "
+                      f"{moves} complete moves in ~{seconds:.0f} s")
+    cal = os.path.join(HERE, "profiles", "r02", "cpu_calibration.json")
+    if os.path.exists(cal):
+        with open(cal) as f:
+            c = json.load(f)
+        r = c["ratio_reference_over_port"]
+        out["calibration"] = dict(ratio_reference_over_port=r, cores=c["cores"], source=os.path.relpath(cal, HERE),
+                                  reference_equivalent=rate * r,
+                                  note="the reference's own multiprocess pipeline vs this port, timed back to back on "
+                                       "the build container's cores; reference_equivalent = value x ratio")
+    return out
 
 
 def main():

@@ -730,29 +730,35 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRng &rng, bool &terr, 
       Board nb2 = b;
       int rew = 0, done = 0;
       const int st = step<G>(nb2, a, player, &rew, &done);
+      if (done) {
+        // terminal: backup (mcts.py:94-98) then remove the path's virtual loss (:365); one lane per
+        // path node (s_node was written by lane 0 of this wave: LDS operations of a wave stay in order)
+        const double val = terminal_value(v, b, rew * player);
+        for (int k = lane; k <= depth; k += P) {
+          const size_t idx = nb + s_node[k];
+          v.bn[idx] += 1;
+          v.bw[idx] += val;
+          if (v.strong) v.bf64[idx] = 1;
+          v.bvl[idx] -= 1;
+        }
+        if (lane == 0) {
+          v.bn[nb + child] += 1;
+          v.bw[nb + child] += val;
+          if (v.strong) v.bf64[nb + child] = 1;
+        }
+      } else {
+        const size_t pb = (size_t)ps * G::MAXD;
+        for (int k = lane; k <= depth; k += P) v.pnode[pb + k] = s_node[k];
+      }
       if (lane == 0) {
         if (st != STEP_OK) set_err(v, SPMCTS_ERR_STATE);
         cnt[C_SIMS] += 1;
         cnt[C_DEPTH] += depth + 1;
         if (done) {
-          // terminal: backup (mcts.py:94-98) then remove the path's virtual loss (:365)
-          const double val = terminal_value(v, b, rew * player);
-          v.bn[nb + child] += 1;
-          v.bw[nb + child] += val;
-          if (v.strong) v.bf64[nb + child] = 1;
-          for (int k = 0; k <= depth; ++k) {
-            const size_t idx = nb + s_node[k];
-            v.bn[idx] += 1;
-            v.bw[idx] += val;
-            if (v.strong) v.bf64[idx] = 1;
-            v.bvl[idx] -= 1;
-          }
           cnt[C_TERM] += 1;
         } else {
-          // lock the leaf (mcts.py:359) and stash the path for the backup
+          // lock the leaf (mcts.py:359); the path was stashed above for the backup
           v.bc[nb + child] = -2;
-          const size_t pb = (size_t)ps * G::MAXD;
-          for (int k = 0; k <= depth; ++k) v.pnode[pb + k] = s_node[k];
           v.plen[ps] = depth + 1;
           v.leaf[ps] = child;
           v.lpos[ps] = nb2.pos;
@@ -1029,20 +1035,24 @@ __global__ __launch_bounds__(64) void k_expand_vl(View v, const float *probs0, c
       v.bf64[ci] = 0;
       v.bvl[ci] = 0;
     }
-    if (lane == 0) {
-      const double val = (double)vrow * (double)v.lmover[ps];
-      v.bvm[bb + blk] = legal_mask<G>(Board{v.lpos[ps], v.lneg[ps]});
-      v.bc[nb + leaf] = blk;
-      v.bn[nb + leaf] += 1;
-      v.bw[nb + leaf] += val;
+    const double val = (double)vrow * (double)v.lmover[ps];
+    {
+      // backup of the path (distinct nodes): one lane per path node, so the read-modify-writes
+      // overlap instead of forming a dependent chain
       const int plen = v.plen[ps];
       const size_t pb = (size_t)ps * G::MAXD;
-      for (int k = 0; k < plen; ++k) {
+      for (int k = lane; k < plen; k += P) {
         const size_t idx = nb + v.pnode[pb + k];
         v.bn[idx] += 1;
         v.bw[idx] += val;
         v.bvl[idx] -= 1;
       }
+    }
+    if (lane == 0) {
+      v.bvm[bb + blk] = legal_mask<G>(Board{v.lpos[ps], v.lneg[ps]});
+      v.bc[nb + leaf] = blk;
+      v.bn[nb + leaf] += 1;
+      v.bw[nb + leaf] += val;
       v.used[tree] = blk + 1;
       v.need[ps] = 0;
       v.cnt[(size_t)tree * C_NCNT + C_NN] += 1;
