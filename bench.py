@@ -258,7 +258,8 @@ def main():
         one_step()
     if D.is_distributed() and args.warmup % args.exchange_every:
         ex.end_ply(eng.stats_vector, force=True)
-    ex._plies = 0  # the timed region starts a fresh episode batch
+    ex._plies = ex.rounds = ex.rows_gathered = 0  # the timed region starts a fresh episode batch
+    ex.seconds = 0.0
     eng.check()
     c0 = eng.counters()
     eng.enable_timers(True)
@@ -415,7 +416,9 @@ def main():
             "nn_ms": nn_ms,
             "share_of_step": nn_ms / 1e3 / elapsed if elapsed else None,
         },
-        "exchange": {"every_plies": args.exchange_every, "rounds": ex.rounds, "rows_to_rank0": ex.rows_gathered},
+        "exchange": {"every_plies": args.exchange_every, "rounds": ex.rounds, "rows_to_rank0": ex.rows_gathered,
+                     "ms_per_round": ex.seconds / max(1, ex.rounds) * 1e3,
+                     "share_of_timed_region": ex.seconds / elapsed if elapsed else None},
         "tree": {
             "sims": sims_all,
             "mean_select_levels": levels_local / max(1, sims_local),

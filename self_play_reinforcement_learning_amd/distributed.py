@@ -24,6 +24,7 @@ backend "nccl" is RCCL on ROCm (xGMI between the GPUs of a node); the same
 code runs on "gloo" for CPU tests.
 """
 import os
+import time
 
 import torch
 import torch.distributed as dist
@@ -185,6 +186,7 @@ class MoveExchange:
         self._plies = 0
         self.rounds = 0
         self.rows_gathered = 0
+        self.seconds = 0.0  # host wall time spent in exchange rounds (this rank)
 
     def stage(self, moves):
         if not is_distributed():
@@ -205,6 +207,13 @@ class MoveExchange:
         return self.exchange(stats_fn() if stats_fn is not None else [], done)
 
     def exchange(self, stats, done):
+        t0 = time.perf_counter()
+        try:
+            return self._exchange(stats, done)
+        finally:
+            self.seconds += time.perf_counter() - t0
+
+    def _exchange(self, stats, done):
         dev = _comm_device()
         world = dist.get_world_size()
         rows = torch.cat(self._staged, 0).to(dev) if self._staged else torch.zeros((0, self.width), dtype=torch.uint8,
