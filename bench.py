@@ -35,7 +35,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 TRAFFIC_FILE = os.path.join(HERE, "profiles", "r01_bench_prof", "k_tower_traffic.json")  # --search-threads 1
-TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r01_bench_prof_k4", "k_tower_traffic.json")  # 4 (default)
+TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r02_bench_prof_k4", "k_tower_traffic.json")  # 4 (default)
 TREE_TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r02_tree_pmc", "tree_traffic.json")
 
 # MI355X reference figures (/opt/skills/guides/MI355X_MICROARCH.md)
@@ -187,8 +187,9 @@ def cpu_baseline(seconds, cores, sims, filter_factor, num_blocks, threads=1, ope
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=8, help="timed plies")
-    ap.add_argument("--warmup", type=int, default=3, help="untimed plies")
+    ap.add_argument("--steps", type=int, default=24, help="timed plies")
+    ap.add_argument("--warmup", type=int, default=24,
+                    help="untimed plies (24 ~ one game generation: games have reached their steady mix of lengths)")
     ap.add_argument("--games", type=int, default=4096, help="concurrent games per GPU")
     ap.add_argument("--sims", type=int, default=200)
     ap.add_argument("--filter-factor", type=int, default=32)
