@@ -26,6 +26,7 @@ evaluated by that network), or "random" / "lookahead" for the hard-coded
 players of games/general/hardcoded_players.py, optionally with its own
 `opponent_iterations`; `record=False` skips Move records (update=False).
 """
+import os
 import time
 
 import torch
@@ -418,7 +419,11 @@ class LanedEngine:
         self.max_games = kw.pop("max_games", None)
         budgets = [None] * lanes if self.max_games is None else \
             [self.max_games // lanes + (1 if i < self.max_games % lanes else 0) for i in range(lanes)]
-        self.streams = [torch.cuda.Stream(device=self.device) for _ in range(lanes)]
+        # SPMCTS_LANE_PRIORITY=1: lane 0's stream at high priority, so its tower workgroups are dispatched
+        # first and the lanes' tree phases fall under each other's towers instead of coinciding
+        prio = os.environ.get("SPMCTS_LANE_PRIORITY", "0") == "1"
+        self.streams = [torch.cuda.Stream(device=self.device, priority=(-1 if prio and i == 0 else 0))
+                        for i in range(lanes)]
         self.lanes = []
         off = 0
         for i, (n, st) in enumerate(zip(sizes, self.streams)):
