@@ -32,6 +32,7 @@
 
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -807,7 +808,7 @@ __global__ __launch_bounds__(64) void k_select_vl(View v, int n_active) {
   __shared__ int32_t s_node[GPB][G::MAXD];
   const int lane = threadIdx.x & (P - 1);
   const int grp = threadIdx.x / P;
-  const int slot = blockIdx.x * GPB + grp;
+  const int slot = blockIdx.x * (int)(blockDim.x / P) + grp;  // blockDim = 64 (GPB trees) or P (one tree)
   if (slot >= n_active) return;
   const int tree = v.active[slot];
   if (tree < 0) return;
@@ -1579,6 +1580,7 @@ struct spmcts_arena {
   View v;
   std::vector<void *> allocs;
   int n_active;  // active-set size for select / search_end
+  int tree_block;  // threads per workgroup of the threaded tree kernels: 64 (64/P trees per wave) or P (one)
 };
 
 static int geometry(const spmcts_config *c, int *A, int *P, int *cells, int *maxd, int *maxm) {
@@ -1818,6 +1820,13 @@ int spmcts_arena_create(const spmcts_config *cfg, int device, spmcts_arena **out
     delete h;
     return rc;
   }
+  {
+    // SPMCTS_TREE_BLOCK=P: one tree per wave in the threaded tree kernels (each tree's dependent chain
+    // runs on its own instead of in lock step with 64/P - 1 others); default 64 threads per workgroup
+    const char *e = getenv("SPMCTS_TREE_BLOCK");
+    const int tb = e ? atoi(e) : 64;
+    h->tree_block = (tb == h->P || tb == 64) ? tb : 64;
+  }
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) {
     delete h;
@@ -1929,7 +1938,8 @@ int spmcts_select_tree(spmcts_arena *h, spmcts_stream stream) {
   if (n > 0) {
     const int gpb = 64 / h->P;
     if (h->v.K > 1) {
-      DISPATCH(h, hipLaunchKernelGGL(k_select_vl<GG>, dim3(nblk(n, gpb)), dim3(64), 0, s, h->v, n));
+      const int tb = h->tree_block, tpb = tb / h->P;
+      DISPATCH(h, hipLaunchKernelGGL(k_select_vl<GG>, dim3(nblk(n, tpb)), dim3(tb), 0, s, h->v, n));
     } else {
       DISPATCH(h, hipLaunchKernelGGL(k_select<GG>, dim3(nblk(n, gpb)), dim3(64), 0, s, h->v, n));
     }
@@ -1957,7 +1967,8 @@ int spmcts_expand2(spmcts_arena *h, const float *probs0_dev, const float *values
     return fail(-1, "two-network arena needs network-1 outputs");
   const int gpb = 64 / h->P;
   if (h->v.K > 1) {
-    DISPATCH(h, hipLaunchKernelGGL(k_expand_vl<GG>, dim3(nblk(h->v.T, gpb)), dim3(64), 0, (hipStream_t)stream, h->v,
+    const int tb = h->tree_block, tpb = tb / h->P;
+    DISPATCH(h, hipLaunchKernelGGL(k_expand_vl<GG>, dim3(nblk(h->v.T, tpb)), dim3(tb), 0, (hipStream_t)stream, h->v,
                                    probs0_dev, values0_dev, probs1_dev, values1_dev));
   } else {
     DISPATCH(h, hipLaunchKernelGGL(k_expand<GG>, dim3(nblk(h->v.T, gpb)), dim3(64), 0, (hipStream_t)stream, h->v,

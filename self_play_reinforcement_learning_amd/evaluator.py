@@ -15,6 +15,7 @@ Supported networks (chosen in `make_evaluator`):
     evaluated row by row (a compatibility path for e.g. InferenceProxy-like
     objects, not a throughput path).
 """
+import logging
 import numpy as np
 import torch
 from torch import nn
@@ -153,6 +154,11 @@ def make_evaluator(network, game, device=None, dtype=torch.bfloat16, leaf_layout
             network.to(device)
         if backend == "hip" or (backend == "auto" and dtype == torch.bfloat16 and HipTowerEvaluator.supported(network)):
             return HipTowerEvaluator(network, device=device)
+        if backend == "auto":
+            logging.getLogger(__name__).info(
+                "fused HIP tower not instantiated for %s x %s boards with %d channels (built: 7x6 / 3x3, C = 128 or "
+                "256): leaf evaluation runs on the PyTorch TowerEvaluator (MIOpen convolutions, %s)",
+                W, H, 4 * int(getattr(network, "filter_factor", 0)), dtype)
         return TowerEvaluator(network, dtype=dtype, leaf_layout=leaf_layout, device=device)
     if isinstance(network, nn.Module):
         if device is not None:
