@@ -656,29 +656,53 @@ __global__ __launch_bounds__(64) void k_select(View v, int n_active) {
 // oracle/mcts.py (OracleTree.search, threads=K) restates exactly this schedule; the G6 fixture
 // (threaded_stats.json) pins its statistics to the reference's own threaded search.
 // ----------------------------------------------------------------------------
-enum { SIM_DONE = 0, SIM_PENDING = 1, SIM_ERROR = -1 };
+enum { SIM_DONE = 0, SIM_PENDING = 1, SIM_LEAK = 2, SIM_ERROR = -1 };
+
+// The searching tree's root, loaded once per kernel and kept in registers across the K fills /
+// backups / refills (it is on every path): node id, its child block (fixed during a search: the
+// root is expanded), board, player, and its visit count and virtual loss, updated in step with the
+// stores every sim and backup makes to them.
+struct TreeRoot {
+  int node, cb, player, n, vl;
+  Board b;
+};
+
+template <class G>
+__device__ __forceinline__ TreeRoot load_root(const View &v, int tree) {
+  const size_t nb = nbase<G>(v, tree);
+  TreeRoot R;
+  R.node = v.root[tree];
+  R.b = Board{v.rpos[tree], v.rneg[tree]};
+  R.player = v.rplayer[tree];
+  R.n = v.bn[nb + R.node];
+  R.vl = v.bvl[nb + R.node];
+  R.cb = v.bc[nb + R.node];
+  return R;
+}
 
 // One search_node with virtual loss (mcts.py:340-367) for pending slot j of `tree`, run by the
 // tree's P-lane group.  vl += 1 on every node passed (mcts.py:345), children scored with
 // q = (w - vl)/(n + vl) and u = c p sqrt(N + vl_parent)/(1 + n + vl) (mcts.py:59-78), pending leaves
 // locked (child-block index -2, score -1e10, mcts.py:86-88).  Returns SIM_PENDING with the leaf
-// locked and its path stashed in slot j, SIM_DONE for a terminal leaf (backed up, path vl removed)
-// or a leak, SIM_ERROR on a corrupt tree.  The return value is uniform across the group.
+// locked and its path stashed in slot j, SIM_DONE for a terminal leaf (backed up, path vl removed),
+// SIM_LEAK for a leak, SIM_ERROR on a corrupt tree; R (the root in registers) is updated to match.
+// The return value is uniform across the group.
 template <class G>
-__device__ int sim_vl(const View &v, int tree, int j, TreeRng &rng, bool &terr, int32_t *s_node, bool noise,
-                      double nz, int64_t *cnt) {
+__device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng, bool &terr, int32_t *s_node,
+                      bool noise, double nz, int64_t *cnt) {
   constexpr int P = G::APAD;
   const int lane = threadIdx.x & (P - 1);
   const int gbase = (threadIdx.x & 63) & ~(P - 1);
   const size_t nb = nbase<G>(v, tree);
   const size_t bb = (size_t)tree * v.cap;
   const int ps = tree * v.K + j;
-  int node = v.root[tree];
-  Board b{v.rpos[tree], v.rneg[tree]};
-  int player = v.rplayer[tree];
-  int node_n = v.bn[nb + node];
-  int node_vl = v.bvl[nb + node] + 1;  // this sim's virtual loss on the node (mcts.py:345)
-  int cb = v.bc[nb + node];
+  int node = R.node;
+  Board b = R.b;
+  int player = R.player;
+  int node_n = R.n;
+  int node_vl = R.vl + 1;  // this sim's virtual loss on the node (mcts.py:345)
+  int cb = R.cb;
+  R.vl += 1;
   int depth = 0;
   for (;;) {
     if (lane == 0) {
@@ -715,7 +739,7 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRng &rng, bool &terr, 
     }
     if (!group_or<P>(valid ? 1 : 0)) {  // mcts.py:349-354: return, virtual loss left in place
       if (lane == 0) cnt[C_LEAK] += 1;
-      return SIM_DONE;
+      return SIM_LEAK;
     }
     double s = -INFINITY;
     if (lane < G::A) s = score + 0.000001 * rng_lane(v, rng, lane, &terr);
@@ -747,6 +771,8 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRng &rng, bool &terr, 
           v.bw[nb + child] += val;
           if (v.strong) v.bf64[nb + child] = 1;
         }
+        R.n += 1;  // the root is s_node[0]
+        R.vl -= 1;
       } else {
         const size_t pb = (size_t)ps * G::MAXD;
         for (int k = lane; k <= depth; k += P) v.pnode[pb + k] = s_node[k];
@@ -787,15 +813,15 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRng &rng, bool &terr, 
 // Refill pending slot j: start sims until one waits for the network or the tree's budget of
 // search_node calls is spent (`started` counts them, mcts.py:328-331 submits `iterations`).
 template <class G>
-__device__ int fill_slot_vl(const View &v, int tree, int j, int limit, int &started, TreeRng &rng, bool &terr,
-                            int32_t *s_node, bool noise, double nz, int64_t *cnt) {
+__device__ int fill_slot_vl(const View &v, int tree, int j, int limit, int &started, TreeRoot &R, TreeRng &rng,
+                            bool &terr, int32_t *s_node, bool noise, double nz, int64_t *cnt) {
   while (started < limit) {
     ++started;
-    const int r = sim_vl<G>(v, tree, j, rng, terr, s_node, noise, nz, cnt);
+    const int r = sim_vl<G>(v, tree, j, R, rng, terr, s_node, noise, nz, cnt);
     // the next sim reads what this one wrote (lane 0's stores, other lanes' loads): one wave owns
     // the tree, so a workgroup-scope fence (stores complete, same CU's L1) is enough
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    if (r != SIM_DONE) return r;
+    if (r == SIM_PENDING || r == SIM_ERROR) return r;
   }
   return SIM_DONE;
 }
@@ -819,11 +845,12 @@ __global__ __launch_bounds__(64) void k_select_vl(View v, int n_active) {
   const double nz = (noise && lane < G::A) ? v.noise[(size_t)tree * P + lane] : 0.0;
   TreeRng rng;
   rng_load(v, tree, rng);
+  TreeRoot R = load_root<G>(v, tree);
   bool terr = false;
   int64_t *cnt = v.cnt + (size_t)tree * C_NCNT;
   for (int j = 0; j < v.K; ++j) {
     if (v.need[tree * v.K + j]) continue;
-    if (fill_slot_vl<G>(v, tree, j, limit, started, rng, terr, s_node[grp], noise, nz, cnt) == SIM_ERROR) return;
+    if (fill_slot_vl<G>(v, tree, j, limit, started, R, rng, terr, s_node[grp], noise, nz, cnt) == SIM_ERROR) return;
   }
   if (lane == 0) {
     v.tstarted[tree] = started;
@@ -995,73 +1022,106 @@ __global__ __launch_bounds__(64) void k_expand_vl(View v, const float *probs0, c
                                                   const float *probs1, const float *values1) {
   constexpr int P = G::APAD;
   constexpr int GPB = 64 / P;
+  constexpr int KMAX = P;  // slots whose records one lane each prefetches (spmcts_arena_create: K <= P)
   __shared__ int32_t s_node[GPB][G::MAXD];
   const int lane = threadIdx.x & (P - 1);
   const int grp = threadIdx.x / P;
+  const int gbase = (threadIdx.x & 63) & ~(P - 1);
   const int tree = (blockIdx.x * blockDim.x + threadIdx.x) / P;
   if (tree >= v.T) return;
+  const int K = v.K;
   const size_t nb = nbase<G>(v, tree);
   const size_t bb = (size_t)tree * v.cap;
+  // prefetch (independent loads, one round trip): lane j < K holds pending slot j's record, every lane
+  // the j-th path node of each slot; the tree's counters
+  const int psl = tree * K + (lane < K ? lane : 0);
+  const int my_need = lane < K ? (int)v.need[psl] : 0;
+  const int my_srow = v.srow[psl], my_leaf = v.leaf[psl], my_plen = v.plen[psl];
+  const int my_mover = v.lmover[psl];
+  const uint64_t my_pos = v.lpos[psl], my_neg = v.lneg[psl];
+  int pnode_r[KMAX];
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j)
+    pnode_r[j] = (j < K && lane < G::MAXD) ? v.pnode[(size_t)(tree * K + j) * G::MAXD + lane] : 0;
+  if (!group_or<P>(my_need)) return;
   const int limit = min(v.budget[tree], v.iters);
   int started = v.tstarted[tree];
   const bool refill = started < limit;
-  bool any = false;
-  for (int j = 0; j < v.K; ++j) any = any || v.need[tree * v.K + j];
-  if (!any) return;
+  int used = v.used[tree];
   const bool noise = v.noise_on[tree] != 0;
   const double nz = (noise && lane < G::A) ? v.noise[(size_t)tree * P + lane] : 0.0;
   TreeRng rng;
-  if (refill) rng_load(v, tree, rng);
+  TreeRoot R;
+  if (refill) {
+    rng_load(v, tree, rng);
+    R = load_root<G>(v, tree);
+  }
+  // the network outputs of the pending slots (second round trip: they depend on the rows)
+  float pr[KMAX], vr[KMAX];
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j) {
+    const int nj = __shfl(my_need, gbase + j, 64), row = __shfl(my_srow, gbase + j, 64);
+    pr[j] = 0.f;
+    vr[j] = 0.f;
+    if (j < K && nj) {
+      const bool s1 = row >= v.seg1;
+      const float *prow = s1 ? probs1 + (size_t)(row - v.seg1) * G::A : probs0 + (size_t)row * G::A;
+      if (lane < G::A) pr[j] = prow[lane];
+      vr[j] = s1 ? values1[row - v.seg1] : values0[row];
+    }
+  }
   bool terr = false;
   int64_t *cnt = v.cnt + (size_t)tree * C_NCNT;
-  for (int j = 0; j < v.K; ++j) {
-    const int ps = tree * v.K + j;
-    if (!v.need[ps]) continue;
-    const int row = v.srow[ps];
-    const bool s1 = row >= v.seg1;
-    const float *prow = s1 ? probs1 + (size_t)(row - v.seg1) * G::A : probs0 + (size_t)row * G::A;
-    const float vrow = s1 ? values1[row - v.seg1] : values0[row];
-    const int blk = v.used[tree];
-    if (blk >= v.cap) {
-      if (lane == 0) set_err(v, SPMCTS_ERR_POOL);
-      return;
-    }
-    const int leaf = v.leaf[ps];
-    {
-      const size_t ci = nb + (size_t)blk * P + lane;
-      v.bn[ci] = 0;
-      v.bw[ci] = 0.0;
-      v.bp[ci] = lane < G::A ? prow[lane] : 0.f;
-      v.bc[ci] = -1;
-      v.bf64[ci] = 0;
-      v.bvl[ci] = 0;
-    }
-    const double val = (double)vrow * (double)v.lmover[ps];
-    {
-      // backup of the path (distinct nodes): one lane per path node, so the read-modify-writes
-      // overlap instead of forming a dependent chain
-      const int plen = v.plen[ps];
-      const size_t pb = (size_t)ps * G::MAXD;
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j) {
+    if (j >= K) break;
+    const int ps = tree * K + j;
+    if (__shfl(my_need, gbase + j, 64)) {
+      const int leaf = __shfl(my_leaf, gbase + j, 64), plen = __shfl(my_plen, gbase + j, 64);
+      const int mover = __shfl(my_mover, gbase + j, 64);
+      const uint64_t lpos = __shfl(my_pos, gbase + j, 64), lneg = __shfl(my_neg, gbase + j, 64);
+      const int blk = used;
+      if (blk >= v.cap) {
+        if (lane == 0) set_err(v, SPMCTS_ERR_POOL);
+        return;
+      }
+      ++used;
+      {
+        const size_t ci = nb + (size_t)blk * P + lane;
+        v.bn[ci] = 0;
+        v.bw[ci] = 0.0;
+        v.bp[ci] = lane < G::A ? pr[j] : 0.f;
+        v.bc[ci] = -1;
+        v.bf64[ci] = 0;
+        v.bvl[ci] = 0;
+      }
+      const double val = (double)vr[j] * (double)mover;
+      // backup of the path (distinct nodes): one lane per path node, the node ids prefetched
       for (int k = lane; k < plen; k += P) {
-        const size_t idx = nb + v.pnode[pb + k];
+        const size_t idx = nb + (k < P ? pnode_r[j] : v.pnode[(size_t)ps * G::MAXD + k]);
         v.bn[idx] += 1;
         v.bw[idx] += val;
         v.bvl[idx] -= 1;
       }
+      if (lane == 0) {
+        v.bvm[bb + blk] = legal_mask<G>(Board{lpos, lneg});
+        v.bc[nb + leaf] = blk;
+        v.bn[nb + leaf] += 1;
+        v.bw[nb + leaf] += val;
+        v.used[tree] = blk + 1;
+        v.need[ps] = 0;
+        cnt[C_NN] += 1;
+        cnt[C_HWM] = max(cnt[C_HWM], (int64_t)(blk + 1));
+      }
+      if (refill && plen > 0) {  // the root is the path's first node
+        R.n += 1;
+        R.vl -= 1;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      if (refill &&
+          fill_slot_vl<G>(v, tree, j, limit, started, R, rng, terr, s_node[grp], noise, nz, cnt) == SIM_ERROR)
+        return;
     }
-    if (lane == 0) {
-      v.bvm[bb + blk] = legal_mask<G>(Board{v.lpos[ps], v.lneg[ps]});
-      v.bc[nb + leaf] = blk;
-      v.bn[nb + leaf] += 1;
-      v.bw[nb + leaf] += val;
-      v.used[tree] = blk + 1;
-      v.need[ps] = 0;
-      v.cnt[(size_t)tree * C_NCNT + C_NN] += 1;
-      v.cnt[(size_t)tree * C_NCNT + C_HWM] = max(v.cnt[(size_t)tree * C_NCNT + C_HWM], (int64_t)(blk + 1));
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    if (refill && fill_slot_vl<G>(v, tree, j, limit, started, rng, terr, s_node[grp], noise, nz, cnt) == SIM_ERROR)
-      return;
   }
   if (refill && lane == 0) {
     v.tstarted[tree] = started;
@@ -1716,6 +1776,7 @@ static int setup_view(spmcts_arena *h, const spmcts_config *cfg) {
   v.leaf_format = cfg->leaf_format;
   v.leaf_layout = cfg->leaf_layout;
   v.K = std::max(1, cfg->search_threads);
+  if (v.K > P) return fail(-3, "search_threads must not exceed the lane group (8 for connect4, 16 for tictactoe)");
   v.iters = std::max(1, cfg->iterations);
   v.NS = v.T * v.K;
   v.seg1 = v.NS;
