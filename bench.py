@@ -345,7 +345,7 @@ def main():
         traffic_src = os.path.relpath(tfile, HERE)
 
     out = {
-        "metric": "self-play positions/sec (Connect4, 200 sims/move)",
+        "metric": f"self-play positions/sec (Connect4, {args.sims} sims/move)",
         "value": moves_all / elapsed_max,
         "unit": "positions/s",
         "n_gpus": world,
