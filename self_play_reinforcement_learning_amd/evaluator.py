@@ -302,6 +302,11 @@ class HipTowerEvaluator(Evaluator):
         leaves: the arena's whole leaf buffer (NCHW view of NHWC bf16 storage, >= max_rows rows);
         count_dev: device int32 holding the row count.  Returns max_rows-row probs/values buffers
         of which the first *count_dev rows are valid (the arena's expand reads the same count)."""
+        self.tower_dev(leaves, count_dev, max_rows)
+        return self.heads_dev(count_dev, max_rows)
+
+    def tower_dev(self, leaves, count_dev, max_rows):
+        """The trunk half of forward_dev (k_tower_dyn) on the current stream."""
         dev = leaves.device
         self.reserve(max_rows, dev)
         feats, probs, values = self._dev_bufs
@@ -319,9 +324,16 @@ class HipTowerEvaluator(Evaluator):
             timer.stop()
         if rc != 0:
             raise self._lib.SpmctsError(f"spmcts_tower_forward_dev failed ({rc})")
-        rc = L.spmcts_tower_heads_dev(self.W, self.H, self.C, self.A, c(feats.data_ptr()), c(count_dev.data_ptr()),
-                                      max_rows, c(self.head_w.data_ptr()), c(self.head_b.data_ptr()),
-                                      c(probs.data_ptr()), c(values.data_ptr()), stream)
+
+    def heads_dev(self, count_dev, max_rows):
+        """The linear-heads half of forward_dev (k_heads) on the current stream."""
+        feats, probs, values = self._dev_bufs
+        c = self._lib.ctypes.c_void_p
+        stream = c(torch.cuda.current_stream().cuda_stream)
+        rc = self._lib.lib().spmcts_tower_heads_dev(self.W, self.H, self.C, self.A, c(feats.data_ptr()),
+                                                    c(count_dev.data_ptr()), max_rows, c(self.head_w.data_ptr()),
+                                                    c(self.head_b.data_ptr()), c(probs.data_ptr()),
+                                                    c(values.data_ptr()), stream)
         if rc != 0:
             raise self._lib.SpmctsError(f"spmcts_tower_heads_dev failed ({rc})")
         return probs, values
