@@ -255,41 +255,11 @@ class SelfPlayEngine:
         sims in flight only the first step launches the select kernel (it fills the K slots); later
         steps' selects run inside the expand kernel, which refills each slot right after its backup
         (the rolling schedule, csrc/spmcts.hip), so they only gather the pending leaves into rows."""
-        X = getattr(self, "tree_stream", None)
-        if X is None or not hasattr(self.evaluator, "tower_dev") or self.evaluator1 is not None:
-            if step == 0 or self.search_threads == 1:
-                self.arena.select_async(self.select_timer)
-            else:
-                self.arena.leaf_rows_async()
-            self._eval_expand_dev(cap=self.n_games * self.search_threads)
-            return
-        # tree stream (SPMCTS_TREE_STREAM, LanedEngine): the tower on this lane's stream M, the tree
-        # kernels and the linear heads on a high-priority stream X, so that when a tower workgroup of
-        # either lane retires, this lane's short, latency-bound kernels take the freed CU first
-        M = torch.cuda.current_stream(self.device)
-        a = self.arena
-        rows = min(a.max_rows, self.n_games * self.search_threads)
-        X.wait_stream(M)
-        with torch.cuda.stream(X):
-            if step == 0 or self.search_threads == 1:
-                a.select_async(self.select_timer)
-            else:
-                a.leaf_rows_async()
-        M.wait_stream(X)
-        if self.nn_timer is not None:
-            self.nn_timer.start()
-        self.evaluator.tower_dev(a.leaves(rows), a.count_dev, rows)
-        X.wait_stream(M)
-        with torch.cuda.stream(X):
-            probs, values = self.evaluator.heads_dev(a.count_dev, rows)
-            if self.nn_timer is not None:
-                self.nn_timer.stop()
-            if self.expand_timer is not None:
-                self.expand_timer.start()
-            a.expand(probs, values)
-            if self.expand_timer is not None:
-                self.expand_timer.stop()
-        M.wait_stream(X)
+        if step == 0 or self.search_threads == 1:
+            self.arena.select_async(self.select_timer)
+        else:
+            self.arena.leaf_rows_async()
+        self._eval_expand_dev(cap=self.n_games * self.search_threads)
 
     def _ply_move(self):
         self.arena.games_end_ply_async()
@@ -454,15 +424,12 @@ class LanedEngine:
         prio = os.environ.get("SPMCTS_LANE_PRIORITY", "0") == "1"
         self.streams = [torch.cuda.Stream(device=self.device, priority=(-1 if prio and i == 0 else 0))
                         for i in range(lanes)]
-        tree_streams = os.environ.get("SPMCTS_TREE_STREAM", "0") == "1"
         self.lanes = []
         off = 0
         for i, (n, st) in enumerate(zip(sizes, self.streams)):
             with torch.cuda.stream(st):
                 self.lanes.append(SelfPlayEngine(game, network, n_games=n, seed=seed, subsequence0=subsequence0 + 2 * off,
                                                  device=self.device, max_games=budgets[i], **kw))
-                if tree_streams:
-                    self.lanes[-1].tree_stream = torch.cuda.Stream(device=self.device, priority=-1)
             off += n
         torch.cuda.synchronize(self.device)
         if lanes > 1 and pack:
