@@ -179,6 +179,14 @@ struct Nbr {
   }
 };
 
+// Channel order in LDS.  A lane's 16 accumulator values of a 32x32 MFMA tile are the output channels
+// ct*32 + 8g + 4h + j (g, j = 0..3, h = lane half); they are stored at the PHYSICAL positions
+// ct*32 + 16h + 4g + j, so that each lane's 16 values are one contiguous 32-byte run (two 16-byte
+// LDS stores instead of four 8-byte ones; the epilogue's store burst is the layer boundary's cost).
+// The next layer's weights are packed with their input channels in the same physical order
+// (evaluator._pack_conv(in_perm=True)), so the MFMAs see consistent K chunks.
+__device__ __forceinline__ int phys_off(int ct, int h, int g) { return (ct * 32 + 16 * h + 4 * g) * 2; }
+
 // Accumulator initialisation: bias (and, for the second conv of a block, the residual input,
 // which lives at the output location in dst) so the epilogue is only ReLU + bf16 + store.
 template <class K, bool RESID>
@@ -195,7 +203,8 @@ __device__ __forceinline__ void acc_init(f32x16 (&acc)[K::MT][K::NT], const char
       for (int t = 0; t < K::NT; ++t) {
         float v0 = bv.x, v1 = bv.y, v2 = bv.z, v3 = bv.w;
         if (RESID) {
-          const bf16x4 x = *(const bf16x4 *)(dst + (((wave / K::CG) * K::NT + t) * 32 + r) * K::RS + ch * 2);
+          const bf16x4 x = *(const bf16x4 *)(dst + (((wave / K::CG) * K::NT + t) * 32 + r) * K::RS +
+                                             phys_off((wave % K::CG) * K::MT + m, h, g));
           v0 += (float)x[0];
           v1 += (float)x[1];
           v2 += (float)x[2];
@@ -223,7 +232,7 @@ __device__ __forceinline__ void acc_store_bias_relu(const f32x16 (&acc)[K::MT][K
       const float4 bv = *(const float4 *)(bias + ch);
 #pragma unroll
       for (int t = 0; t < K::NT; ++t) {
-        char *p = dst + (((wave / K::CG) * K::NT + t) * 32 + r) * K::RS + ch * 2;
+        char *p = dst + (((wave / K::CG) * K::NT + t) * 32 + r) * K::RS + phys_off((wave % K::CG) * K::MT + m, h, g);
         float v0 = acc[m][t][4 * g + 0] + bv.x, v1 = acc[m][t][4 * g + 1] + bv.y;
         float v2 = acc[m][t][4 * g + 2] + bv.z, v3 = acc[m][t][4 * g + 3] + bv.w;
         if (RESID) {
@@ -257,40 +266,45 @@ template <class K, bool RESID>
 __device__ __forceinline__ void acc_store_bias_relu_pre(const f32x16 (&acc)[K::MT][K::NT], char *dst,
                                                         const float4 (&bv)[K::MT][4], int wave, int lane) {
   const int r = lane & 31, h = lane >> 5;
-  // per channel tile m: the residuals (block input) of its 4 x NT output groups are read in one batch
+  // per channel tile m: the residuals (block input) of its NT output runs are read in one batch
   // before any of them is written, so the LDS latency is paid once per batch instead of once per
-  // read -> add -> write chain (one batch per m keeps the staging at 2 x NT x 4 registers)
+  // read -> add -> write chain; each run is the lane's 16 channels, contiguous (phys_off)
 #pragma unroll
   for (int m = 0; m < K::MT; ++m) {
-    bf16x4 res[RESID ? 4 : 1][K::NT];
+    const int ct = (wave % K::CG) * K::MT + m;
+    uint4 res[RESID ? K::NT : 1][2];
     if constexpr (RESID) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
-#pragma unroll
-        for (int t = 0; t < K::NT; ++t)
-          res[g][t] = *(const bf16x4 *)(dst + (((wave / K::CG) * K::NT + t) * 32 + r) * K::RS +
-                                        (((wave % K::CG) * K::MT + m) * 32 + 8 * g + 4 * h) * 2);
+      for (int t = 0; t < K::NT; ++t) {
+        const char *p = dst + (((wave / K::CG) * K::NT + t) * 32 + r) * K::RS + phys_off(ct, h, 0);
+        res[t][0] = *(const uint4 *)p;
+        res[t][1] = *(const uint4 *)(p + 16);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int ch = ((wave % K::CG) * K::MT + m) * 32 + 8 * g + 4 * h;
+    for (int t = 0; t < K::NT; ++t) {
+      char *p = dst + (((wave / K::CG) * K::NT + t) * 32 + r) * K::RS + phys_off(ct, h, 0);
+      uint32_t o[8];
 #pragma unroll
-      for (int t = 0; t < K::NT; ++t) {
-        char *p = dst + (((wave / K::CG) * K::NT + t) * 32 + r) * K::RS + ch * 2;
+      for (int g = 0; g < 4; ++g) {
         float v0 = acc[m][t][4 * g + 0] + bv[m][g].x, v1 = acc[m][t][4 * g + 1] + bv[m][g].y;
         float v2 = acc[m][t][4 * g + 2] + bv[m][g].z, v3 = acc[m][t][4 * g + 3] + bv[m][g].w;
         if constexpr (RESID) {
-          const bf16x4 x = res[g][t];
-          v0 += (float)x[0];
-          v1 += (float)x[1];
-          v2 += (float)x[2];
-          v3 += (float)x[3];
+          const uint32_t x0 = ((const uint32_t *)&res[t][g >> 1])[2 * (g & 1)];
+          const uint32_t x1 = ((const uint32_t *)&res[t][g >> 1])[2 * (g & 1) + 1];
+          v0 += __uint_as_float(x0 << 16);
+          v1 += __uint_as_float(x0 & 0xffff0000u);
+          v2 += __uint_as_float(x1 << 16);
+          v3 += __uint_as_float(x1 & 0xffff0000u);
         }
         // ReLU on the converted bf16 pairs (v_cvt_pk_bf16_f32 + v_pk_max_i16: identical bits to
         // converting max(v, 0), one instruction per pair instead of one per value)
-        *(uint2 *)p = make_uint2(relu_pk_bf16(f32x2{v0, v1}), relu_pk_bf16(f32x2{v2, v3}));
+        o[2 * g] = relu_pk_bf16(f32x2{v0, v1});
+        o[2 * g + 1] = relu_pk_bf16(f32x2{v2, v3});
       }
+      *(uint4 *)p = make_uint4(o[0], o[1], o[2], o[3]);
+      *(uint4 *)(p + 16) = make_uint4(o[4], o[5], o[6], o[7]);
     }
   }
 }
@@ -312,7 +326,7 @@ __device__ __forceinline__ void acc_store_bias_relu_pk(const f32x16 (&acc)[K::MT
       const f32x2 b01 = {bv.x, bv.y}, b23 = {bv.z, bv.w};
 #pragma unroll
       for (int t = 0; t < K::NT; ++t) {
-        char *p = dst + (((wave / K::CG) * K::NT + t) * 32 + r) * K::RS + ch * 2;
+        char *p = dst + (((wave / K::CG) * K::NT + t) * 32 + r) * K::RS + phys_off((wave % K::CG) * K::MT + m, h, g);
         f32x2 lo = f32x2{acc[m][t][4 * g + 0], acc[m][t][4 * g + 1]} + b01;
         f32x2 hi = f32x2{acc[m][t][4 * g + 2], acc[m][t][4 * g + 3]} + b23;
         if (RESID) {
@@ -340,7 +354,7 @@ __device__ __forceinline__ void acc_store_relu(const f32x16 (&acc)[K::MT][K::NT]
         o[1] = (__bf16)fmaxf(acc[m][t][4 * g + 1], 0.f);
         o[2] = (__bf16)fmaxf(acc[m][t][4 * g + 2], 0.f);
         o[3] = (__bf16)fmaxf(acc[m][t][4 * g + 3], 0.f);
-        *(bf16x4 *)(dst + (((wave / K::CG) * K::NT + t) * 32 + r) * K::RS + ch * 2) = o;
+        *(bf16x4 *)(dst + (((wave / K::CG) * K::NT + t) * 32 + r) * K::RS + phys_off((wave % K::CG) * K::MT + m, h, g)) = o;
       }
     }
 }

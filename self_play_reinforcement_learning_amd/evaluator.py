@@ -171,9 +171,22 @@ def make_evaluator(network, game, device=None, dtype=torch.bfloat16, leaf_layout
 
 
 # ----------------------------------------------------------------------------- fused HIP tower
-def _pack_conv(w, cin_pad=None):
-    """[Cout][Cin][kh][kw] fp -> bf16 fragments [Cout/32][taps][Cin/16][64 lanes][8] (csrc/tower.hip)."""
+def phys_channel_order(c):
+    """Logical channel held at each PHYSICAL LDS position of the fused tower's activations
+    (csrc/tower.hip phys_off): within every 32-channel tile, position 16h + 4g + j holds the MFMA
+    output row 8g + 4h + j."""
+    p = torch.arange(c)
+    w = p % 32
+    return (p - w) + 8 * ((w % 16) // 4) + 4 * (w // 16) + w % 4
+
+
+def _pack_conv(w, cin_pad=None, in_perm=False):
+    """[Cout][Cin][kh][kw] fp -> bf16 fragments [Cout/32][taps][Cin/16][64 lanes][8] (csrc/tower.hip).
+    in_perm: the layer reads activations another tower layer wrote, which sit in the physical channel
+    order (phys_channel_order), so the input-channel axis is permuted to match."""
     cout, cin, kh, kw = w.shape
+    if in_perm:
+        w = w[:, phys_channel_order(cin).to(w.device)]
     if cin_pad is not None and cin_pad > cin:
         w = torch.cat([w, torch.zeros(cout, cin_pad - cin, kh, kw, dtype=w.dtype, device=w.device)], 1)
         cin = cin_pad
@@ -232,11 +245,11 @@ class HipTowerEvaluator(Evaluator):
         for blk in t.residual_blocks:
             for conv, bn in ((blk.conv1, blk.bn1), (blk.conv2, blk.bn2)):
                 w, b = fold(conv, bn)
-                ws.append(_pack_conv(w))
+                ws.append(_pack_conv(w, in_perm=True))
                 bs.append(b)
         wp, bp = fold(t.conv_policy, t.policy_bn)
         wv, bv = fold(t.conv_value, t.value_bn)
-        ws.append(_pack_conv(torch.cat([wp, wv], 0)))
+        ws.append(_pack_conv(torch.cat([wp, wv], 0), in_perm=True))
         bs.append(torch.cat([bp, bv], 0))
         self.n_blocks = len(t.residual_blocks)
         self.wblob = torch.cat(ws).to(dev).contiguous()
