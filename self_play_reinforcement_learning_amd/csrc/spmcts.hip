@@ -30,6 +30,8 @@
 #include <rocrand/rocrand_philox4x32_10.h>
 #include <rocrand/rocrand_uniform.h>
 
+#include "philox.h"
+
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -178,10 +180,16 @@ __device__ __forceinline__ void rng_load(const View &v, int tree, TreeRng &r) {
 }
 
 __device__ __forceinline__ void rng_store(const View &v, int tree, const TreeRng &r) {
-  if (v.rng_mode == SPMCTS_RNG_TAPE)
+  if (v.rng_mode == SPMCTS_RNG_TAPE) {
     v.tape_cur[tree] = r.cur;
-  else
-    v.rng[tree] = r.st;
+  } else {
+    // rng_advance moved only the counter / substate: refresh rocRAND's output block (philox.h)
+    Philox s = r.st;
+    PhiloxFields f = philox_fields(s);
+    philox_sync(f);
+    philox_put(s, f);
+    v.rng[tree] = s;
+  }
 }
 
 // One double in [0, 1) for lane `j` of a k-wide vector draw (all lanes call it with the
@@ -195,16 +203,19 @@ __device__ __forceinline__ double rng_lane(const View &v, const TreeRng &r, int 
     }
     return v.tape[i];
   }
-  Philox s = r.st;
-  skipahead(2ull * (unsigned long long)j, &s);
-  return 1.0 - rocrand_uniform_double(&s);  // rocRAND gives (0, 1]
+  // = skipahead(2j) + rocrand_uniform_double, without the run-time index into the output block
+  return 1.0 - philox_uniform_at(philox_fields(r.st), 2ull * (unsigned long long)j);  // rocRAND gives (0, 1]
 }
 
 __device__ __forceinline__ void rng_advance(const View &v, TreeRng &r, int k) {
-  if (v.rng_mode == SPMCTS_RNG_TAPE)
+  if (v.rng_mode == SPMCTS_RNG_TAPE) {
     r.cur += k;
-  else
-    skipahead(2ull * (unsigned long long)k, &r.st);
+  } else {
+    // skipahead(2k) minus its output-block refresh (rng_store does that once)
+    PhiloxFields f = philox_fields(r.st);
+    philox_skip(f, 2ull * (unsigned long long)k);
+    philox_put(r.st, f);
+  }
 }
 
 // sequential scalar draw (single thread)
@@ -1024,6 +1035,11 @@ __global__ __launch_bounds__(64) void k_expand_vl(View v, const float *probs0, c
   constexpr int GPB = 64 / P;
   constexpr int KMAX = P;  // slots whose records one lane each prefetches (spmcts_arena_create: K <= P)
   __shared__ int32_t s_node[GPB][G::MAXD];
+  // the prefetched path nodes (k < P) and network outputs of each slot, per tree group; each LDS word
+  // is written and later read by the same wave (LDS operations of a wave stay in order)
+  __shared__ int32_t s_pnode[GPB][KMAX][P];
+  __shared__ float s_pr[GPB][KMAX][P];
+  __shared__ float s_vr[GPB][KMAX];
   const int lane = threadIdx.x & (P - 1);
   const int grp = threadIdx.x / P;
   const int gbase = (threadIdx.x & 63) & ~(P - 1);
@@ -1039,10 +1055,14 @@ __global__ __launch_bounds__(64) void k_expand_vl(View v, const float *probs0, c
   const int my_srow = v.srow[psl], my_leaf = v.leaf[psl], my_plen = v.plen[psl];
   const int my_mover = v.lmover[psl];
   const uint64_t my_pos = v.lpos[psl], my_neg = v.lneg[psl];
-  int pnode_r[KMAX];
+  {
+    int pn[KMAX];
 #pragma unroll
-  for (int j = 0; j < KMAX; ++j)
-    pnode_r[j] = (j < K && lane < G::MAXD) ? v.pnode[(size_t)(tree * K + j) * G::MAXD + lane] : 0;
+    for (int j = 0; j < KMAX; ++j)
+      pn[j] = (j < K && lane < G::MAXD) ? v.pnode[(size_t)(tree * K + j) * G::MAXD + lane] : 0;
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) s_pnode[grp][j][lane] = pn[j];
+  }
   if (!group_or<P>(my_need)) return;
   const int limit = min(v.budget[tree], v.iters);
   int started = v.tstarted[tree];
@@ -1057,24 +1077,32 @@ __global__ __launch_bounds__(64) void k_expand_vl(View v, const float *probs0, c
     R = load_root<G>(v, tree);
   }
   // the network outputs of the pending slots (second round trip: they depend on the rows)
-  float pr[KMAX], vr[KMAX];
+  {
+    float pr[KMAX], vr[KMAX];
 #pragma unroll
-  for (int j = 0; j < KMAX; ++j) {
-    const int nj = __shfl(my_need, gbase + j, 64), row = __shfl(my_srow, gbase + j, 64);
-    pr[j] = 0.f;
-    vr[j] = 0.f;
-    if (j < K && nj) {
-      const bool s1 = row >= v.seg1;
-      const float *prow = s1 ? probs1 + (size_t)(row - v.seg1) * G::A : probs0 + (size_t)row * G::A;
-      if (lane < G::A) pr[j] = prow[lane];
-      vr[j] = s1 ? values1[row - v.seg1] : values0[row];
+    for (int j = 0; j < KMAX; ++j) {
+      const int nj = __shfl(my_need, gbase + j, 64), row = __shfl(my_srow, gbase + j, 64);
+      pr[j] = 0.f;
+      vr[j] = 0.f;
+      if (j < K && nj) {
+        const bool s1 = row >= v.seg1;
+        const float *prow = s1 ? probs1 + (size_t)(row - v.seg1) * G::A : probs0 + (size_t)row * G::A;
+        if (lane < G::A) pr[j] = prow[lane];
+        vr[j] = s1 ? values1[row - v.seg1] : values0[row];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+      s_pr[grp][j][lane] = pr[j];
+      if (lane == 0) s_vr[grp][j] = vr[j];
     }
   }
   bool terr = false;
   int64_t *cnt = v.cnt + (size_t)tree * C_NCNT;
-#pragma unroll
-  for (int j = 0; j < KMAX; ++j) {
-    if (j >= K) break;
+  // one copy of the slot body (a rolled loop: the unrolled form was 70 KB of code, more than the
+  // instruction cache two CUs share, for a kernel that runs one wave per CU on a latency chain)
+#pragma unroll 1
+  for (int j = 0; j < K; ++j) {
     const int ps = tree * K + j;
     if (__shfl(my_need, gbase + j, 64)) {
       const int leaf = __shfl(my_leaf, gbase + j, 64), plen = __shfl(my_plen, gbase + j, 64);
@@ -1090,15 +1118,15 @@ __global__ __launch_bounds__(64) void k_expand_vl(View v, const float *probs0, c
         const size_t ci = nb + (size_t)blk * P + lane;
         v.bn[ci] = 0;
         v.bw[ci] = 0.0;
-        v.bp[ci] = lane < G::A ? pr[j] : 0.f;
+        v.bp[ci] = lane < G::A ? s_pr[grp][j][lane] : 0.f;
         v.bc[ci] = -1;
         v.bf64[ci] = 0;
         v.bvl[ci] = 0;
       }
-      const double val = (double)vr[j] * (double)mover;
+      const double val = (double)s_vr[grp][j] * (double)mover;
       // backup of the path (distinct nodes): one lane per path node, the node ids prefetched
       for (int k = lane; k < plen; k += P) {
-        const size_t idx = nb + (k < P ? pnode_r[j] : v.pnode[(size_t)ps * G::MAXD + k]);
+        const size_t idx = nb + (k < P ? s_pnode[grp][j][k] : v.pnode[(size_t)ps * G::MAXD + k]);
         v.bn[idx] += 1;
         v.bw[idx] += val;
         v.bvl[idx] -= 1;

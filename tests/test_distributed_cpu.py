@@ -18,6 +18,28 @@ def _free_port():
     return tempfile.mkdtemp(prefix="spmcts_dist_") + "/store"
 
 
+def _by_value(obj):
+    """Tensors -> numpy for a result queue: torch shares CPU tensors through file descriptors that the
+    sending process must outlive, and the rank workers exit right after putting their results."""
+    if isinstance(obj, torch.Tensor):
+        return ("__t__", obj.detach().cpu().numpy())
+    if isinstance(obj, dict):
+        return {k: _by_value(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_by_value(v) for v in obj)
+    return obj
+
+
+def _restore(obj):
+    if isinstance(obj, tuple) and len(obj) == 2 and isinstance(obj[0], str) and obj[0] == "__t__":
+        return torch.from_numpy(obj[1])
+    if isinstance(obj, dict):
+        return {k: _restore(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_restore(v) for v in obj)
+    return obj
+
+
 def _moves(rank, n):
     g = torch.Generator().manual_seed(rank)
     return dict(
@@ -41,8 +63,8 @@ def _worker(rank, world, port, q):
     with torch.no_grad():
         net.weight.fill_(float(rank))
     D.broadcast_state_dict(net)
-    q.put((rank, stats.tolist(), None if got is None else {k: v.clone() for k, v in got.items()}, mx,
-           float(net.weight.sum())))
+    q.put(_by_value((rank, stats.tolist(), None if got is None else {k: v.clone() for k, v in got.items()}, mx,
+                     float(net.weight.sum()))))
     torch.distributed.destroy_process_group()
 
 
@@ -103,7 +125,7 @@ def _loop_worker(rank, world, port, q):
     eng = _FakeEngine(rate=rank + 1, rank=rank)
     gathered = []
     plies = SelfPlayEngine.play_games(eng, 6, on_moves=lambda m: gathered.append(m["game"].tolist()), every=4)
-    q.put((rank, plies, eng.games_done, gathered))
+    q.put(_by_value((rank, plies, eng.games_done, gathered)))
     torch.distributed.destroy_process_group()
 
 
@@ -118,7 +140,7 @@ def test_play_games_keeps_ranks_in_step_gloo(world):
     procs = [ctx.Process(target=_loop_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=120) for _ in procs], key=lambda x: x[0])
+    res = sorted([_restore(q.get(timeout=120)) for _ in procs], key=lambda x: x[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -176,7 +198,7 @@ def _laned_worker(rank, world, port, q):
     eng.device = torch.device("cpu")
     games = []
     plies = eng.play_games(8, on_moves=lambda m: games.extend(m["game"].tolist()), every=2)
-    q.put((rank, plies, [ln.games_done for ln in eng.lanes], games))
+    q.put(_by_value((rank, plies, [ln.games_done for ln in eng.lanes], games)))
     torch.distributed.destroy_process_group()
 
 
@@ -191,7 +213,7 @@ def test_laned_engine_play_games_gloo():
     procs = [ctx.Process(target=_laned_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=120) for _ in procs], key=lambda x: x[0])
+    res = sorted([_restore(q.get(timeout=120)) for _ in procs], key=lambda x: x[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -220,7 +242,7 @@ def test_exchange_primitives_gloo(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=120) for _ in procs], key=lambda x: x[0])
+    res = sorted([_restore(q.get(timeout=120)) for _ in procs], key=lambda x: x[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -246,7 +268,7 @@ def _exchange_worker(rank, world, port, q):
         ex.stage(_moves(10 * rank + ply, (rank + ply) % 3))  # 0..2 records per ply, some plies none
         out.append(ex.end_ply(lambda: [rank, ply], done=ply >= 2 + rank))
     out.append(ex.end_ply(lambda: [rank, 99], done=True, force=True))
-    q.put((rank, out, got, ex.rounds))
+    q.put(_by_value((rank, out, got, ex.rounds)))
     torch.distributed.destroy_process_group()
 
 
@@ -261,7 +283,7 @@ def test_move_exchange_rounds_gloo(world):
     procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=120) for _ in procs], key=lambda x: x[0])
+    res = sorted([_restore(q.get(timeout=120)) for _ in procs], key=lambda x: x[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
