@@ -129,9 +129,10 @@ __device__ __forceinline__ bf16x8 lds_b128(const char *p) { return *(const bf16x
 struct WBuf {
   __amdgpu_buffer_rsrc_t rsrc;
   int voff;
+  template <int AUX = 0>
   __device__ __forceinline__ bf16x8 load(uint32_t byte_off) const {
     typedef int i32x4 __attribute__((ext_vector_type(4)));
-    const i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, (int)byte_off, 0);
+    const i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, (int)byte_off, AUX);
     return __builtin_bit_cast(bf16x8, v);
   }
 };
@@ -563,6 +564,8 @@ __device__ __forceinline__ void conv_tap_x(const char *src, const Nbr<K> &nb, f3
   constexpr int STEPS = 9 * KK;
   constexpr uint32_t LV = X::lt(TAP);
   constexpr uint32_t LVN = TAP < 8 ? X::lt(TAP < 8 ? TAP + 1 : 8) : 0u;
+  // weight-load cache policy (timing variants: ABL 4096 = sc0, 8192 = nt, 16384 = sc1)
+  constexpr int WAUX = (K::ABL & 4096) ? 1 : (K::ABL & 8192) ? 2 : (K::ABL & 16384) ? 16 : 0;
   constexpr int NTA = (int)X::popc(LV);
   static_assert(NTA >= 1 && K::MT * NTA >= NTA + K::MT, "schedule: enough MFMAs for the loads");
   if constexpr (TAP < 8) {
@@ -573,7 +576,10 @@ __device__ __forceinline__ void conv_tap_x(const char *src, const Nbr<K> &nb, f3
 #pragma unroll
   for (int kk = 0; kk < KK; ++kk) {
     const int s = TAP * KK + kk;
-    if (kk + 1 < KK) {
+    if constexpr (K::ABL & 8) {  // timing ablation: no LDS operand reads
+#pragma unroll
+      for (int t = 0; t < K::NT; ++t) bn[t] = bc[t];
+    } else if (kk + 1 < KK) {
 #pragma unroll
       for (int t = 0; t < K::NT; ++t)
         if ((LV >> t) & 1u) bn[t] = lds_b128(src + off_cur[t] + (kk + 1) * 32);
@@ -587,12 +593,20 @@ __device__ __forceinline__ void conv_tap_x(const char *src, const Nbr<K> &nb, f3
 #pragma unroll
     for (int m = 0; m < K::MT; ++m) acur[m] = a[slot][m];
     const int sn = s + DEPTH;
-    if (sn < STEPS) {
+    if constexpr (K::ABL & 16) {  // timing ablation: no weight loads (the ring is reused)
+    } else if constexpr ((K::ABL & 512) && MG_ == 1) {  // timing ablation: row half 1 skips its loads
+    } else if constexpr (K::ABL & 128) {  // timing ablation: half the weight bytes (m = 0 only)
+      if (sn < STEPS) a[slot][0] = wb.load(wl_off + (uint32_t)sn * 1024u);
+      else if (sn - STEPS < wn_steps) a[slot][0] = wb.load(wn_off + (uint32_t)(sn - STEPS) * 1024u);
 #pragma unroll
-      for (int m = 0; m < K::MT; ++m) a[slot][m] = wb.load(wl_off + m * MSTRIDE + (uint32_t)sn * 1024u);
+      for (int m = 1; m < K::MT; ++m) a[slot][m] = a[slot][0];
+    } else if (sn < STEPS) {
+#pragma unroll
+      for (int m = 0; m < K::MT; ++m) a[slot][m] = wb.template load<WAUX>(wl_off + m * MSTRIDE + (uint32_t)sn * 1024u);
     } else if (sn - STEPS < wn_steps) {
 #pragma unroll
-      for (int m = 0; m < K::MT; ++m) a[slot][m] = wb.load(wn_off + m * MSTRIDE + (uint32_t)(sn - STEPS) * 1024u);
+      for (int m = 0; m < K::MT; ++m)
+        a[slot][m] = wb.template load<WAUX>(wn_off + m * MSTRIDE + (uint32_t)(sn - STEPS) * 1024u);
     }
     if (TAP == 0 && kk == 0) {
 #pragma unroll
@@ -726,6 +740,10 @@ __device__ __forceinline__ void conv_layer_x(const char *src, char *dst, const N
       if (((K::EDGE ? X::ZPRE_T : X::ZPRE) >> t) & 1u) acc[m][t] = f32x16{};
   int off_cur[K::NT], off_nxt[K::NT];
   bf16x8 bc[K::NT], bn[K::NT];
+  if constexpr (K::ABL & 8) {
+#pragma unroll
+    for (int t = 0; t < K::NT; ++t) bc[t] = lds_b128(src + nb.off(t, 0) + hoff);
+  }
 #pragma unroll
   for (int t = 0; t < K::NT; ++t)
     if (((K::EDGE ? X::lt(0) : X::LIVE[0]) >> t) & 1u) {
@@ -736,7 +754,11 @@ __device__ __forceinline__ void conv_layer_x(const char *src, char *dst, const N
 #define TAPX(T) conv_tap_x<K, KK, DEPTH, MG_, T>(src, nb, acc, bc, bn, off_cur, off_nxt, a, hoff, wb, wl_off, wn_off, wn_steps)
     TAPX(0); TAPX(1); TAPX(2); TAPX(3); TAPX(4); TAPX(5); TAPX(6); TAPX(7); TAPX(8);
 #undef TAPX
-    acc_store_bias_relu_pre<K, RESID>(acc, dst, bv, wave, lane);
+    if constexpr (K::ABL & 2) {  // timing ablation: no epilogue (a never-true test keeps the MFMAs live)
+      if (bv[0][0].x == 12345.f) acc_store_bias_relu_pre<K, RESID>(acc, dst, bv, wave, lane);
+    } else {
+      acc_store_bias_relu_pre<K, RESID>(acc, dst, bv, wave, lane);
+    }
     return;
   }
   conv_group_x<K, KK, DEPTH, MG_, 0>(src, nb, acc, bc, bn, off_cur, off_nxt, a, hoff, wb, wl_off, wn_off, wn_steps);
@@ -897,7 +919,8 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
     }
     const int wn_steps = L + 1 < n_convs ? LSTEPS : 0;
     if constexpr (K::XMAJ) {
-      static_assert(K::MG == 2 && K::ABL == 0, "column-group conv: two row halves, no ablations");
+      static_assert(K::MG == 2 && (K::ABL & ~(2 | 4 | 8 | 16 | 128 | 512 | 4096 | 8192 | 16384)) == 0 && (K::ABL == 0 || K::EDGE),
+                    "column-group conv: two row halves; edge tiles take the 2/4/8/16/128 timing ablations");
       const bool even = (L & 1) == 0;
       if (wave / K::CG == 0) {
         if (even) conv_layer_x<K, KK, DEPTH, false, 0>(X, Y, nb, ring, b, wave, lane, wb, wl_off, wn_off, wn_steps);
@@ -1246,6 +1269,15 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
       ABLATE(0) ABLATE(1) ABLATE(2) ABLATE(4) ABLATE(8) ABLATE(16) ABLATE(24) ABLATE(31) ABLATE(64) ABLATE(128)
       ABLATE(256) ABLATE(2048) ABLATE(32768)
 #undef ABLATE
+#define ABLATE_EDGE(X) \
+      case 200 + X: return launch<Cfg<128, 256, 7, 6, 2, 4, X, 4, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      ABLATE_EDGE(0) ABLATE_EDGE(2) ABLATE_EDGE(4) ABLATE_EDGE(6) ABLATE_EDGE(8) ABLATE_EDGE(16) ABLATE_EDGE(24)
+      ABLATE_EDGE(30) ABLATE_EDGE(128) ABLATE_EDGE(512)
+      case 301: return launch<Cfg<128, 256, 7, 6, 2, 4, 4096, 4, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      case 302: return launch<Cfg<128, 256, 7, 6, 2, 4, 8192, 4, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      case 316: return launch<Cfg<128, 256, 7, 6, 2, 4, 16384, 4, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+#undef ABLATE_EDGE
+      case 250: return launch<Cfg<128, 256, 7, 6, 2, 4, 0, 8, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);  // ring depth 8
       case 10: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);  // two tile sizes only
       case 15: return launch_split<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true>, Cfg<128, 192, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);  // column-major tiles without edge rows
       case 11: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 192, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);  // board-major full tiles
