@@ -838,10 +838,10 @@ __device__ int fill_slot_vl(const View &v, int tree, int j, int limit, int &star
 }
 
 // First step of a search: fill the K slots of every searching tree.
-template <class G>
-__global__ __launch_bounds__(64) void k_select_vl(View v, int n_active) {
+template <class G, int TB = 64>
+__global__ __launch_bounds__(TB) void k_select_vl(View v, int n_active) {
   constexpr int P = G::APAD;
-  constexpr int GPB = 64 / P;
+  constexpr int GPB = TB / P;
   __shared__ int32_t s_node[GPB][G::MAXD];
   const int lane = threadIdx.x & (P - 1);
   const int grp = threadIdx.x / P;
@@ -1028,11 +1028,11 @@ __global__ __launch_bounds__(64) void k_expand(View v, const float *probs0, cons
 // earlier slots of the same tree have changed the shared ancestors.  Pending leaves of trees that
 // are not searching (a _set_node expansion, slot 0, path length 0) are completed without a refill.
 // ----------------------------------------------------------------------------
-template <class G>
-__global__ __launch_bounds__(64) void k_expand_vl(View v, const float *probs0, const float *values0,
+template <class G, int TB = 64>
+__global__ __launch_bounds__(TB) void k_expand_vl(View v, const float *probs0, const float *values0,
                                                   const float *probs1, const float *values1) {
   constexpr int P = G::APAD;
-  constexpr int GPB = 64 / P;
+  constexpr int GPB = TB / P;
   constexpr int KMAX = P;  // slots whose records one lane each prefetches (spmcts_arena_create: K <= P)
   __shared__ int32_t s_node[GPB][G::MAXD];
   // the prefetched path nodes (k < P) and network outputs of each slot, per tree group; each LDS word
@@ -1910,11 +1910,13 @@ int spmcts_arena_create(const spmcts_config *cfg, int device, spmcts_arena **out
     return rc;
   }
   {
-    // SPMCTS_TREE_BLOCK=P: one tree per wave in the threaded tree kernels (each tree's dependent chain
-    // runs on its own instead of in lock step with 64/P - 1 others); default 64 threads per workgroup
+    // Threads per workgroup of the threaded tree kernels (SPMCTS_TREE_BLOCK): P = one tree per wave,
+    // 64 = one wave of 64/P trees, 128..512 = 2..8 such waves.  A tree-kernel wave (~170 VGPRs) leaves no
+    // room on its SIMD for a trunk wave (416 registers), so each tree workgroup keeps a whole CU away from
+    // the other lane's trunk launch while it runs: fewer, fuller workgroups block fewer CUs.
     const char *e = getenv("SPMCTS_TREE_BLOCK");
     const int tb = e ? atoi(e) : 64;
-    h->tree_block = (tb == h->P || tb == 64) ? tb : 64;
+    h->tree_block = (tb == h->P || (tb >= 64 && tb <= 512 && tb % 64 == 0)) ? tb : 64;
   }
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) {
@@ -2028,7 +2030,10 @@ int spmcts_select_tree(spmcts_arena *h, spmcts_stream stream) {
     const int gpb = 64 / h->P;
     if (h->v.K > 1) {
       const int tb = h->tree_block, tpb = tb / h->P;
-      DISPATCH(h, hipLaunchKernelGGL(k_select_vl<GG>, dim3(nblk(n, tpb)), dim3(tb), 0, s, h->v, n));
+      if (tb > 64)
+        DISPATCH(h, hipLaunchKernelGGL((k_select_vl<GG, 512>), dim3(nblk(n, tpb)), dim3(tb), 0, s, h->v, n));
+      else
+        DISPATCH(h, hipLaunchKernelGGL(k_select_vl<GG>, dim3(nblk(n, tpb)), dim3(tb), 0, s, h->v, n));
     } else {
       DISPATCH(h, hipLaunchKernelGGL(k_select<GG>, dim3(nblk(n, gpb)), dim3(64), 0, s, h->v, n));
     }
@@ -2057,8 +2062,12 @@ int spmcts_expand2(spmcts_arena *h, const float *probs0_dev, const float *values
   const int gpb = 64 / h->P;
   if (h->v.K > 1) {
     const int tb = h->tree_block, tpb = tb / h->P;
-    DISPATCH(h, hipLaunchKernelGGL(k_expand_vl<GG>, dim3(nblk(h->v.T, tpb)), dim3(tb), 0, (hipStream_t)stream, h->v,
-                                   probs0_dev, values0_dev, probs1_dev, values1_dev));
+    if (tb > 64)
+      DISPATCH(h, hipLaunchKernelGGL((k_expand_vl<GG, 512>), dim3(nblk(h->v.T, tpb)), dim3(tb), 0, (hipStream_t)stream,
+                                     h->v, probs0_dev, values0_dev, probs1_dev, values1_dev));
+    else
+      DISPATCH(h, hipLaunchKernelGGL(k_expand_vl<GG>, dim3(nblk(h->v.T, tpb)), dim3(tb), 0, (hipStream_t)stream, h->v,
+                                     probs0_dev, values0_dev, probs1_dev, values1_dev));
   } else {
     DISPATCH(h, hipLaunchKernelGGL(k_expand<GG>, dim3(nblk(h->v.T, gpb)), dim3(64), 0, (hipStream_t)stream, h->v,
                                    probs0_dev, values0_dev, probs1_dev, values1_dev));
