@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "spmcts.h"
 #include "tower_edge.h"
@@ -1123,6 +1124,129 @@ __global__ __launch_bounds__(256) void k_heads(const __bf16 *feats, int n, const
   }
 }
 
+// k_heads with room beside a trunk workgroup.  The trunk holds 152.5 KB of a CU's 160 KB LDS and
+// 416 of each SIMD's 512 registers per lane, so k_heads (86 KB of staged features) could only run on
+// a CU no trunk workgroup occupies: its 512 workgroups waited for the other lane's trunk workgroups
+// to retire (0.8-1 ms per call in the bench against 11 us alone), and the lane's expand and next
+// trunk launch waited behind it.  This form reads the features straight from global memory (L2:
+// the trunk wrote them just before) as the MFMA A operand, fills all 32 MFMA rows with boards (32
+// per workgroup, half the weight traffic of 16), keeps only the cross-wave sums in LDS (4.6 KB), and
+// is held to 96 registers per lane, so one wave fits on each SIMD beside a trunk wave.  Same math
+// in the same order as k_heads (per-wave k order, fixed-order cross-wave sums): bit-identical.
+template <int FF, int CELLS, int A>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_heads_co(
+    const __bf16 *feats, int n, const int32_t *count, const bf16x8 *wf, const float *hb, float *probs, float *values) {
+  using H = HeadsCfg<FF, CELLS, A>;
+  constexpr int BOARDS = 32;
+  if (count) n = min(*count, n);  // n = the caller's buffer rows
+  const int b0 = blockIdx.x * BOARDS;
+  if (b0 >= n) return;
+  __shared__ float s_part[4][BOARDS];     // per-wave value partial sums
+  constexpr int AP = (A + 7) / 8 * 8;
+  __shared__ float s_pol[4][BOARDS][AP];  // per-wave policy partial logits
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int nb = min(BOARDS, n - b0);
+  const float *bp = hb, *bv = hb + 32, *wo = hb + 32 + H::HID, *bo = hb + 32 + 2 * H::HID;
+  // row r = board b0 + r (rows past the batch repeat its last board; their results are not stored)
+  const char *frow = (const char *)feats + (size_t)(b0 + min(r, nb - 1)) * H::FROW;
+  // value tiles first, then the policy quarter (each in k_heads' per-wave k order): only one set of
+  // accumulators is live at a time, which keeps the wave inside 96 registers without spills
+  f32x16 acc[H::VTW];
+#pragma unroll
+  for (int v = 0; v < H::VTW; ++v) acc[v] = f32x16{};
+  constexpr int D = 2;  // weight ring depth
+  bf16x8 ring[D][H::VTW];
+  const bf16x8 *wv = wf + (size_t)(1 + wave * H::VTW) * H::KS * 64 + lane;
+  const bf16x8 *wp = wf + lane;
+  const int q0 = wave * H::KQ, q1 = min(H::KS, q0 + H::KQ);
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+#pragma unroll
+    for (int v = 0; v < H::VTW; ++v) ring[d][v] = wv[((size_t)v * H::KS + d) * 64];
+  // the features of step s (value half at FF, policy half at 0), one step ahead
+  auto feat = [&](int s, int half) {
+    const int k0 = 16 * s + 8 * h;
+    return *(const bf16x8 *)(frow + ((k0 / FF) * 2 * FF + half + k0 % FF) * 2);
+  };
+  bf16x8 avn = feat(0, FF);
+  for (int s0 = 0; s0 < H::KS; s0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int s = s0 + d;
+      if (s >= H::KS) break;
+      const bf16x8 av = avn;
+      if (s + 1 < H::KS) avn = feat(s + 1, FF);
+      bf16x8 wcur[H::VTW];
+#pragma unroll
+      for (int v = 0; v < H::VTW; ++v) {
+        wcur[v] = ring[d][v];
+        if (s + D < H::KS) ring[d][v] = wv[((size_t)v * H::KS + s + D) * 64];
+      }
+#pragma unroll
+      for (int v = 0; v < H::VTW; ++v) acc[v] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, wcur[v], acc[v], 0, 0, 0);
+    }
+  }
+  // value: relu(acc + bv[col]) * wo[col], summed over the hidden units (cols); as k_heads
+  float part[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) part[i] = 0.f;
+#pragma unroll
+  for (int v = 0; v < H::VTW; ++v) {
+    const int col = (wave * H::VTW + v) * 32 + r;
+    const float bb = bv[col], ww = wo[col];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) part[i] += fmaxf(acc[v][i] + bb, 0.f) * ww;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    float x = part[i];
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) x += __shfl_xor(x, off, 32);
+    part[i] = x;
+  }
+  if (r == 0) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s_part[wave][(i & 3) + 8 * (i >> 2) + 4 * h] = part[i];
+  }
+  f32x16 pacc = {};
+  if (q0 < q1) {
+    bf16x8 pn = wp[(size_t)q0 * 64], apn = feat(q0, 0);
+    for (int s = q0; s < q1; ++s) {
+      const bf16x8 pw = pn, ap = apn;
+      if (s + 1 < q1) {
+        pn = wp[(size_t)(s + 1) * 64];
+        apn = feat(s + 1, 0);
+      }
+      pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap, pw, pacc, 0, 0, 0);
+    }
+  }
+  if (r < A) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s_pol[wave][(i & 3) + 8 * (i >> 2) + 4 * h][r] = pacc[i];
+  }
+  __syncthreads();
+  if (tid < nb) {
+    const int bd = b0 + tid;
+    values[bd] = tanhf(((s_part[0][tid] + s_part[1][tid]) + (s_part[2][tid] + s_part[3][tid])) + bo[0]);
+    float lg[A];
+    float m = -INFINITY;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      lg[a] = ((s_pol[0][tid][a] + s_pol[1][tid][a]) + (s_pol[2][tid][a] + s_pol[3][tid][a])) + bp[a];
+      m = fmaxf(m, lg[a]);
+    }
+    float e[A], sum = 0.f;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      e[a] = __expf(lg[a] - m);
+      sum += e[a];
+    }
+    const float inv = 1.f / sum;
+#pragma unroll
+    for (int a = 0; a < A; ++a) probs[(size_t)bd * A + a] = e[a] * inv;
+  }
+}
+
 // Head epilogue after one GEMM  Z = features[n][cells*2ff] @ Wc^T  (Wc = value rows [8ff]
 // then policy rows [A], zero where a row meets the other head's channels):
 //   value = tanh(sum_j relu(Z[j] + bv[j]) * wo[j] + bo), probs = softmax(Z[8ff + a] + bp[a]).
@@ -1299,11 +1423,21 @@ static int tower_heads(int32_t width, int32_t height, int32_t channels, int32_t 
   using namespace tower;
   hipStream_t s = (hipStream_t)stream;
   if (batch <= 0) return batch < 0 ? -3 : 0;
+  // SPMCTS_HEADS=lds: the LDS-staged k_heads (A/B switch, read per call); default the co-resident k_heads_co
+  const char *he = getenv("SPMCTS_HEADS");
+  const int co = (he && strcmp(he, "lds") == 0) ? 0 : 1;
 #define HEADS(FF, CELLS, A)                                                                                   \
-  hipLaunchKernelGGL((k_heads<FF, CELLS, A>), dim3((batch + HeadsCfg<FF, CELLS, A>::BOARDS - 1) /             \
-                                                   HeadsCfg<FF, CELLS, A>::BOARDS), dim3(256), 0, s,           \
-                     (const __bf16 *)features_dev, batch, count_dev, (const bf16x8 *)head_w_dev, head_b_dev,    \
-                     probs_dev, values_dev)
+  do {                                                                                                        \
+  if (co && FF == 32) /* FF = 64 (C = 256) would spill at 96 registers; no room beside that trunk anyway */ \
+    hipLaunchKernelGGL((k_heads_co<FF, CELLS, A>), dim3((batch + 31) / 32), dim3(256), 0, s,                  \
+                       (const __bf16 *)features_dev, batch, count_dev, (const bf16x8 *)head_w_dev, head_b_dev,  \
+                       probs_dev, values_dev);                                                                \
+  else                                                                                                        \
+    hipLaunchKernelGGL((k_heads<FF, CELLS, A>), dim3((batch + HeadsCfg<FF, CELLS, A>::BOARDS - 1) /           \
+                                                     HeadsCfg<FF, CELLS, A>::BOARDS), dim3(256), 0, s,         \
+                         (const __bf16 *)features_dev, batch, count_dev, (const bf16x8 *)head_w_dev, head_b_dev,  \
+                       probs_dev, values_dev);                                                                \
+  } while (0)
   if (width == 7 && height == 6 && actions == 7 && channels == 128)
     HEADS(32, 42, 7);
   else if (width == 7 && height == 6 && actions == 7 && channels == 256)

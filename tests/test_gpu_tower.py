@@ -136,3 +136,23 @@ def test_zero_and_maximum_rows():
     assert (probs[64:] == -7.0).all() and (values[64:] == -7.0).all()
     ref_p, ref_v = hip(x)
     assert torch.equal(probs[:64], ref_p) and torch.equal(values[:64].view(-1), ref_v.view(-1))
+
+
+@pytest.mark.parametrize("game,n", [("connect4", 1), ("connect4", 31), ("connect4", 33), ("connect4", 1000),
+                                    ("connect4", 4096), ("tictactoe", 77)])
+def test_coresident_heads_match_lds_heads(game, n, monkeypatch):
+    """k_heads_co (features read from global memory, 32 boards per workgroup, 96 registers: fits beside
+    a trunk workgroup) gives the LDS-staged k_heads' results bit for bit: same per-wave k order, same
+    fixed-order cross-wave sums; ragged tails (n % 32) read only live boards."""
+    W, H, A = (7, 6, 7) if game == "connect4" else (3, 3, 9)
+    net = _net(W, H, A, 2, 32)
+    x = _planes(W, H, n, seed=11).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    hip = HipTowerEvaluator(net)
+    monkeypatch.setenv("SPMCTS_HEADS", "lds")
+    p0, v0 = hip(x)
+    torch.cuda.synchronize()
+    monkeypatch.delenv("SPMCTS_HEADS")
+    p1, v1 = hip(x)
+    torch.cuda.synchronize()
+    assert torch.equal(p0, p1) and torch.equal(v0, v1)
+    assert torch.isfinite(p1).all() and torch.isfinite(v1).all()
