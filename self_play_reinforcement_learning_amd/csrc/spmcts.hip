@@ -166,7 +166,7 @@ __device__ __forceinline__ size_t nbase(const View &v, int tree) {
 // RNG: Philox (rocRAND) or parity tape
 // ----------------------------------------------------------------------------
 struct TreeRng {
-  Philox st;
+  PhiloxFields f;  // Philox mode: counter, key, substate (f.result is not carried; rng_store rebuilds it)
   int64_t cur, end;
 };
 
@@ -175,7 +175,8 @@ __device__ __forceinline__ void rng_load(const View &v, int tree, TreeRng &r) {
     r.cur = v.tape_cur[tree];
     r.end = v.tape_end[tree];
   } else {
-    r.st = v.rng[tree];
+    // memcpy: the rocRAND object read as its leading fields, without a type-punned access
+    __builtin_memcpy(&r.f, (const void *)(v.rng + tree), sizeof(PhiloxFields));
   }
 }
 
@@ -183,12 +184,11 @@ __device__ __forceinline__ void rng_store(const View &v, int tree, const TreeRng
   if (v.rng_mode == SPMCTS_RNG_TAPE) {
     v.tape_cur[tree] = r.cur;
   } else {
-    // rng_advance moved only the counter / substate: refresh rocRAND's output block (philox.h)
-    Philox s = r.st;
-    PhiloxFields f = philox_fields(s);
+    // the state's leading fields, with rocRAND's output block rebuilt (philox.h); its Box-Muller
+    // cache (the trailing fields, used only by the Dirichlet draws) is left as it was
+    PhiloxFields f = r.f;
     philox_sync(f);
-    philox_put(s, f);
-    v.rng[tree] = s;
+    __builtin_memcpy((void *)(v.rng + tree), &f, sizeof(PhiloxFields));
   }
 }
 
@@ -204,18 +204,14 @@ __device__ __forceinline__ double rng_lane(const View &v, const TreeRng &r, int 
     return v.tape[i];
   }
   // = skipahead(2j) + rocrand_uniform_double, without the run-time index into the output block
-  return 1.0 - philox_uniform_at(philox_fields(r.st), 2ull * (unsigned long long)j);  // rocRAND gives (0, 1]
+  return 1.0 - philox_uniform_at(r.f, 2ull * (unsigned long long)j);  // rocRAND gives (0, 1]
 }
 
 __device__ __forceinline__ void rng_advance(const View &v, TreeRng &r, int k) {
-  if (v.rng_mode == SPMCTS_RNG_TAPE) {
+  if (v.rng_mode == SPMCTS_RNG_TAPE)
     r.cur += k;
-  } else {
-    // skipahead(2k) minus its output-block refresh (rng_store does that once)
-    PhiloxFields f = philox_fields(r.st);
-    philox_skip(f, 2ull * (unsigned long long)k);
-    philox_put(r.st, f);
-  }
+  else
+    philox_skip(r.f, 2ull * (unsigned long long)k);  // skipahead(2k) minus its output-block refresh
 }
 
 // sequential scalar draw (single thread)
@@ -294,27 +290,31 @@ __device__ __forceinline__ double terminal_value(const View &v, Board parent, in
 // Dirichlet root noise (add_noise, mcts.py:49-53): A components, invalid children included.
 template <class G>
 __device__ void draw_noise(const View &v, int tree) {
-  TreeRng r;
-  rng_load(v, tree, r);
   double g[G::A];
   if (v.rng_mode == SPMCTS_RNG_TAPE) {
+    TreeRng r;
+    rng_load(v, tree, r);
     bool terr = false;
     for (int j = 0; j < G::A; ++j) g[j] = rng_lane(v, r, j, &terr);
     rng_advance(v, r, G::A);
     if (terr) set_err(v, SPMCTS_ERR_TAPE);
+    rng_store(v, tree, r);
   } else {
+    // rocRAND's own Gamma path on the whole state (Box-Muller cache included); stores keep its
+    // invariant result == philox10(counter), so the state is rocRAND-consistent here
+    Philox st = v.rng[tree];
     double acc = 0.0;
     for (int j = 0; j < G::A; ++j) {
-      g[j] = gamma_draw(&r.st, v.alpha);
+      g[j] = gamma_draw(&st, v.alpha);
       acc += g[j];
     }
     const double inv = acc > 0.0 ? 1.0 / acc : 0.0;
     for (int j = 0; j < G::A; ++j) g[j] *= inv;
+    v.rng[tree] = st;
   }
   for (int j = 0; j < G::A; ++j) v.noise[(size_t)tree * G::APAD + j] = g[j];
   v.noise_on[tree] = 1;
   v.tstarted[tree] = 0;  // a search begins: `iterations` search_node calls to start
-  rng_store(v, tree, r);
 }
 
 // ----------------------------------------------------------------------------
