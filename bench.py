@@ -201,6 +201,9 @@ def main():
     ap.add_argument("--exchange-every", type=int, default=8,
                     help="plies per episode-batch exchange round (Move rows to rank 0 + stats all-reduce)")
     ap.add_argument("--mode", choices=["selfplay", "arena"], default="selfplay")
+    ap.add_argument("--no-leaf-dedup", action="store_true",
+                    help="evaluate every pending leaf in its own row (default: one row per distinct position "
+                         "of a simulation step, include/spmcts.h spmcts_set_leaf_dedup)")
     ap.add_argument("--lanes", type=int, default=2,
                     help="arenas per GPU on their own HIP streams (engine.LanedEngine); 1 = one arena")
     ap.add_argument("--blocks-per-tree", type=int, default=0,
@@ -240,7 +243,7 @@ def main():
         opponent = ResidualTower(7, 6, 7, num_blocks=args.blocks, filter_factor=args.filter_factor).to(dev).eval()
     kw = dict(iterations=args.sims, seed=1234 + rank, device=dev, bucket=args.bucket, opponent=opponent,
               evaluate=arena_mode, record=not arena_mode, search_threads=args.search_threads,
-              blocks_per_tree=args.blocks_per_tree)
+              blocks_per_tree=args.blocks_per_tree, leaf_dedup=False if args.no_leaf_dedup else None)
     if args.lanes > 1:
         eng = LanedEngine("connect4", net, n_games=args.games, lanes=args.lanes, pack=not args.no_pack, **kw)
     else:
@@ -314,7 +317,9 @@ def main():
 
     # ---- network (MFMA) share: busy time = union of the network launches of all lanes
     nn_ms = union_ms(eng.nn_timer.intervals(ref))
-    rows = c1["nn_leaves"] - c0["nn_leaves"]
+    # rows the network actually evaluated (with leaf dedup, one per distinct position of a step)
+    rows = c1["nn_rows"] - c0["nn_rows"]
+    leaves = c1["nn_leaves"] - c0["nn_leaves"]
     fpl = resnet_flops_per_leaf(7, 6, 7, args.filter_factor, args.blocks)
     nn_tflops = rows * fpl / (nn_ms / 1e3) / 1e12 if nn_ms > 0 else 0.0
     # ---- dominant kernel: k_tower (HIP events around each tower dispatch on its lane's stream).
@@ -367,6 +372,7 @@ def main():
             "parallelism": f"dp{world}",
             "lanes_per_gpu": max(1, args.lanes),
             "search_threads": args.search_threads,
+            "leaf_dedup": bool(getattr(eng, "leaf_dedup", False)),
         },
         "roofline": {
             "kernel": f"tower::k_tower_dyn (fused ResNet-{4 * args.filter_factor}x{args.blocks} trunk, bf16 MFMA)",
@@ -414,6 +420,9 @@ def main():
             "frac": nn_tflops / BF16_DENSE_PEAK_TFLOPS,
             "flops_per_leaf": fpl,
             "rows": rows,
+            "leaves": leaves,
+            "leaf_dedup": bool(getattr(eng, "leaf_dedup", False)),
+            "rows_per_leaf": rows / max(1, leaves),
             "nn_ms": nn_ms,
             "share_of_step": nn_ms / 1e3 / elapsed if elapsed else None,
         },

@@ -110,6 +110,7 @@ typedef struct spmcts_counters {
                                   (mcts.py:349-354); sims + leaked_sims = searches x iterations */
   int64_t compactions;         /* subtree recyclings (node-store compactions before a search; only
                                   when blocks_per_tree is below the worst case)                 */
+  int64_t nn_rows;             /* network rows emitted (= nn_leaves unless leaf dedup is on)  */
 } spmcts_counters;
 
 /* ---- library ------------------------------------------------------------ */
@@ -172,6 +173,14 @@ int spmcts_arena_segments(const spmcts_arena *h, int32_t *seg1);
 int spmcts_set_root_prior_net(spmcts_arena *h, int32_t net, const float *probs_dev, spmcts_stream stream);
 /* Games mode: keep Move records (play_episode update=True, the default) or not (evaluation games). */
 int spmcts_games_set_record(spmcts_arena *h, int32_t record);
+/* Batch leaf dedup (search_threads > 1 only; no effect with 1): pending leaves whose
+ * network input is the same ((own, opp) stones from the mover's view, same network) share one
+ * leaf row, so each distinct position of a simulation step is evaluated once and every leaf reads
+ * its row's outputs.  The reference evaluates each leaf separately (InferenceWorker,
+ * inference_worker.py:89-119); with a deterministic, batch-independent evaluator the outputs each
+ * leaf receives are unchanged.  Off by default; leave it off for evaluators that give rows of
+ * different trees different networks (per-row salts).  Leaf counts then count rows, not leaves. */
+int spmcts_set_leaf_dedup(spmcts_arena *h, int32_t on);
 /* MCTreeSearch._play (mcts.py:272-299) for the active trees + remove_noise:
  * visit-count^(1/temp) distribution, np.random.choice semantics, Move record.
  * Outputs per active tree i: actions_dev[i], states_dev[i][W*H] (int8, tree

@@ -68,6 +68,7 @@ class Counters(ctypes.Structure):
         ("reserved", ctypes.c_uint32),
         ("leaked_sims", ctypes.c_int64),
         ("compactions", ctypes.c_int64),
+        ("nn_rows", ctypes.c_int64),
     ]
 
     def as_dict(self):
@@ -118,6 +119,7 @@ _SIGS = {
     "spmcts_env_step_host": [_I32, _I32, _I32, _P, _I32, _I32, ctypes.POINTER(_I32), ctypes.POINTER(_I32)],
     "spmcts_valid_moves_host": [_I32, _I32, _I32, _P, _P],
     "spmcts_table_net": [_I32, _I32, _I32, _P, _I32, _I32, _I32, _U64, _P, _P, _P, _P],
+    "spmcts_set_leaf_dedup": [_P, _I32],
     "spmcts_leaf_trees": [_P, _P, _P],
     "spmcts_copy_probe": [_P, _P, _U64, _P],
     "spmcts_tower_forward": [_I32, _I32, _I32, _I32, _P, _I32, _P, _P, _P, _P],

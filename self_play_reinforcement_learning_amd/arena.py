@@ -181,6 +181,13 @@ class Arena:
     def games_set_record(self, record=True):
         call("spmcts_games_set_record", self.h, int(bool(record)))
 
+    def set_leaf_dedup(self, on=True):
+        """One leaf row per distinct network input of a simulation step (search_threads > 1;
+        include/spmcts.h spmcts_set_leaf_dedup).  Only for evaluators that are a pure function of the
+        leaf planes (the ResNet evaluators), not for per-row salted table nets."""
+        call("spmcts_set_leaf_dedup", self.h, int(bool(on)))
+        self.leaf_dedup = bool(on) and self.search_threads > 1
+
     def set_tapes(self, tapes):
         """Parity mode: one flat float64 stream per tree (list indexed by tree id)."""
         offs = np.zeros(self.n_trees + 1, dtype=np.int64)

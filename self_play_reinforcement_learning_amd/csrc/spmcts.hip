@@ -120,6 +120,12 @@ struct View {
   int32_t *row_tree;  // row -> pending slot (tree * K + j)
   int32_t *srow;      // pending slot -> row (K > 1)
   int32_t *row_count;
+  // batch leaf dedup (K > 1, spmcts_set_leaf_dedup): pending leaves with the same network input share
+  // one row.  dtab: open-addressing table of (generation << 32 | owner slot), dent: a slot's entry
+  uint64_t *dtab;
+  int32_t *dent;
+  int dedup, dmask;
+  uint32_t dgen;
   float *root_prior;
   uint32_t *err;
   // games
@@ -875,6 +881,76 @@ __global__ __launch_bounds__(TB) void k_select_vl(View v, int n_active) {
 // Two segments: leaves of network-0 trees in rows [0, n0), of network-1 trees in rows
 // [seg1, seg1 + n1) (single-network arenas: seg1 = T, n1 = 0).
 // count_out (optional): [0] = n0 + n1, [1] = n0, [2] = n1.
+// ----------------------------------------------------------------------------
+// batch leaf dedup (K > 1): the network input of a pending leaf is its (own, opp) stone planes from
+// the mover's view (k_encode), so leaves with equal (own, opp) of the same network get one row and
+// one evaluation; the trunk and heads are deterministic and batch-independent, so every leaf still
+// receives exactly the outputs its own row would have produced.  Owner of a key = its lowest slot
+// (deterministic); the table is cleared by generation stamps instead of a memset per step.
+// ----------------------------------------------------------------------------
+template <class G>
+__device__ __forceinline__ void leaf_key(const View &v, int t, uint64_t &own, uint64_t &opp) {
+  const int mover = v.lmover[t];
+  own = mover > 0 ? v.lpos[t] : v.lneg[t];
+  opp = mover > 0 ? v.lneg[t] : v.lpos[t];
+  if (v.tnet[t / v.K]) own |= 1ull << 63;  // rows of the two networks never merge (cell bits < 63)
+}
+
+__device__ __forceinline__ uint32_t leaf_hash(uint64_t a, uint64_t b) {
+  uint64_t x = a ^ (b * 0x9E3779B97F4A7C15ull);
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+
+template <class G>
+__global__ __launch_bounds__(256) void k_dedup_insert(View v) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= v.NS || !v.need[t]) return;
+  uint64_t own, opp;
+  leaf_key<G>(v, t, own, opp);
+  const unsigned long long mine = ((unsigned long long)v.dgen << 32) | (uint32_t)t;
+  unsigned long long *tab = (unsigned long long *)v.dtab;
+  uint32_t h = leaf_hash(own, opp) & (uint32_t)v.dmask;
+  for (int probe = 0; probe <= v.dmask; ++probe) {
+    // claim the entry if it holds an older generation; a failed CAS returns the current value, which
+    // during this kernel can only have become this generation's (at most two rounds)
+    unsigned long long w = tab[h];
+    while ((uint32_t)(w >> 32) != v.dgen) {
+      const unsigned long long old = atomicCAS(tab + h, w, mine);
+      if (old == w) {
+        v.dent[t] = (int)h;
+        return;
+      }
+      w = old;
+    }
+    uint64_t so, sp;
+    leaf_key<G>(v, (int)(uint32_t)w, so, sp);
+    if (so == own && sp == opp) {
+      atomicMin(tab + h, mine);  // the lowest slot of the key owns the row
+      v.dent[t] = (int)h;
+      return;
+    }
+    h = (h + 1) & (uint32_t)v.dmask;
+  }
+  set_err(v, SPMCTS_ERR_STATE);  // unreachable: the table has >= 2 NS entries
+}
+
+__device__ __forceinline__ bool row_owner(const View &v, int t) {
+  return v.need[t] && (!v.dedup || (int)(uint32_t)v.dtab[v.dent[t]] == t);
+}
+
+// duplicates read their owner's row
+__global__ __launch_bounds__(256) void k_dedup_alias(View v) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= v.NS || !v.need[t]) return;
+  const int s = (int)(uint32_t)v.dtab[v.dent[t]];
+  if (s != t) v.srow[t] = v.srow[s];
+}
+
 __global__ __launch_bounds__(1024) void k_scan_need(View v, int32_t *count_out) {
   __shared__ int32_t s_p0[1024], s_p1[1024];
   const int tid = threadIdx.x;
@@ -883,7 +959,7 @@ __global__ __launch_bounds__(1024) void k_scan_need(View v, int32_t *count_out) 
   const int lo = min(T, tid * chunk), hi = min(T, lo + chunk);
   int c0 = 0, c1 = 0;
   for (int t = lo; t < hi; ++t)
-    if (v.need[t]) {
+    if (row_owner(v, t)) {
       if (v.tnet[t / v.K]) ++c1; else ++c0;
     }
   s_p0[tid] = c0;
@@ -900,7 +976,7 @@ __global__ __launch_bounds__(1024) void k_scan_need(View v, int32_t *count_out) 
   }
   int r0 = s_p0[tid] - c0, r1 = v.seg1 + s_p1[tid] - c1;
   for (int t = lo; t < hi; ++t)
-    if (v.need[t]) {
+    if (row_owner(v, t)) {
       const int r = v.tnet[t / v.K] ? r1++ : r0++;
       v.row_tree[r] = t;
       if (v.K > 1) v.srow[t] = r;
@@ -908,6 +984,7 @@ __global__ __launch_bounds__(1024) void k_scan_need(View v, int32_t *count_out) 
   if (tid == 1023) {
     v.row_count[0] = s_p0[1023];
     v.row_count[1] = s_p1[1023];
+    v.gcnt[10] += s_p0[1023] + s_p1[1023];  // network rows emitted (counters.nn_rows)
     if (count_out) {
       count_out[0] = s_p0[1023] + s_p1[1023];
       count_out[1] = s_p0[1023];
@@ -1747,6 +1824,13 @@ static void plan_arena(spmcts_arena *h, Plan &pl) {
   pl.add(&v.row_tree, NS);
   pl.add(&v.srow, NS);
   pl.add(&v.row_count, 4);
+  {
+    size_t tab = 1;
+    while (tab < 2 * NS) tab <<= 1;
+    v.dmask = (int)(tab - 1);
+    pl.add(&v.dtab, v.K > 1 ? tab : 1);
+    pl.add(&v.dent, v.K > 1 ? NS : 1);
+  }
   pl.add(&v.root_prior, 32);  // [net][16]
   pl.add(&v.err, 4);
   pl.add(&v.gpos, G);
@@ -1936,6 +2020,7 @@ int spmcts_arena_create(const spmcts_config *cfg, int device, spmcts_arena **out
     h->allocs.push_back(p);
     *it.first = p;
   }
+  if (h->v.K > 1) (void)hipMemset(h->v.dtab, 0, sizeof(uint64_t) * ((size_t)h->v.dmask + 1));  // generation 0
   hipLaunchKernelGGL(k_rng_init, dim3(nblk(h->v.T, 256)), dim3(256), 0, 0, h->v, cfg->seed, cfg->subsequence0);
   hipLaunchKernelGGL(k_games_init, dim3(nblk(std::max(1, h->v.G), 256)), dim3(256), 0, 0, h->v);
   // default root prior: uniform (replaced by spmcts_set_root_prior)
@@ -2013,7 +2098,12 @@ int spmcts_search_begin(spmcts_arena *h, const int32_t *trees_dev, int32_t n, sp
 }
 
 static int launch_rows(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_dev, hipStream_t s) {
+  if (h->v.dedup) {
+    if (++h->v.dgen == 0) ++h->v.dgen;  // generation 0 = the zeroed table
+    DISPATCH(h, hipLaunchKernelGGL(k_dedup_insert<GG>, dim3(nblk(h->v.NS, 256)), dim3(256), 0, s, h->v));
+  }
   hipLaunchKernelGGL(k_scan_need, dim3(1), dim3(1024), 0, s, h->v, leaf_count_dev);
+  if (h->v.dedup) hipLaunchKernelGGL(k_dedup_alias, dim3(nblk(h->v.NS, 256)), dim3(256), 0, s, h->v);
   if (leaves_dev) {
     const long long total = (long long)h->v.NS * h->cells;
     DISPATCH(h, hipLaunchKernelGGL(k_encode<GG>, dim3(nblk(total, 256)), dim3(256), 0, s, h->v, leaves_dev));
@@ -2119,6 +2209,12 @@ int spmcts_set_root_prior_net(spmcts_arena *h, int32_t net, const float *probs_d
   if (net < 0 || net > 1) return fail(-3, "network index must be 0 or 1");
   HIP_TRY(hipMemcpyAsync(h->v.root_prior + 16 * net, probs_dev, sizeof(float) * h->A, hipMemcpyDeviceToDevice,
                          (hipStream_t)stream));
+  return 0;
+}
+
+int spmcts_set_leaf_dedup(spmcts_arena *h, int32_t on) {
+  if (!h) return fail(-1, "null arena");
+  h->v.dedup = (on && h->v.K > 1) ? 1 : 0;  // K = 1 keeps one row per tree (k_expand walks rows)
   return 0;
 }
 
@@ -2293,6 +2389,7 @@ int spmcts_get_counters(spmcts_arena *h, spmcts_counters *out) {
   out->games_finished = g[0];
   for (int k = 0; k < 6; ++k) out->results[k / 3][k % 3] = g[1 + k];
   out->positions_exported = g[9];
+  out->nn_rows = g[10];
   HIP_TRY(hipMemcpy(&out->error_flags, h->v.err, 4, hipMemcpyDeviceToHost));
   return 0;
 }

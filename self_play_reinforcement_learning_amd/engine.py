@@ -87,7 +87,7 @@ class SelfPlayEngine:
     def __init__(self, game, network, n_games=4096, iterations=200, alpha=1.0, strong_play=False, evaluate=False,
                  seed=0, subsequence0=None, rng="philox", max_games=None, device=None, dtype=torch.bfloat16,
                  leaf_layout="nhwc", cpuct=4.0, x_noise=0.25, blocks_per_tree=0, bucket=256, opponent=None,
-                 opponent_iterations=None, record=True, search_threads=1):
+                 opponent_iterations=None, record=True, search_threads=1, leaf_dedup=None):
         self.game = game
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.evaluator = make_evaluator(network, game, device=self.device, dtype=dtype, leaf_layout=leaf_layout)
@@ -126,6 +126,13 @@ class SelfPlayEngine:
                                         budgets=[iterations, it1] * n_games)
         if not record:
             self.arena.games_set_record(False)
+        # batch leaf dedup (include/spmcts.h spmcts_set_leaf_dedup): one row per distinct position of a
+        # simulation step; by default on when every evaluator is a pure, batch-independent function of
+        # the leaf planes (the fused HIP trunk), so each leaf still gets exactly its own outputs
+        pure = all(getattr(ev, "pure_planes", False) for ev in (self.evaluator, self.evaluator1) if ev is not None)
+        self.leaf_dedup = bool(pure if leaf_dedup is None else leaf_dedup) and self.search_threads > 1
+        if self.leaf_dedup:
+            self.arena.set_leaf_dedup(True)
         self.n_games = n_games
         self.max_games = max_games
         # torch convolutions want few distinct shapes; the fused HIP tower takes any batch
@@ -441,6 +448,7 @@ class LanedEngine:
         self.iterations = self.lanes[0].iterations
         self.select_steps = self.lanes[0].select_steps
         self.search_threads = self.lanes[0].search_threads
+        self.leaf_dedup = self.lanes[0].leaf_dedup
         self.evaluator = self.lanes[0].evaluator
         self.select_timer = self.expand_timer = self.nn_timer = self.tower_timer = None
 

@@ -205,6 +205,13 @@ class HipTowerEvaluator(Evaluator):
     1344->A + softmax, value 1344->8ff->1 + tanh) run as bf16 GEMMs in torch.
     """
 
+    @property
+    def pure_planes(self):
+        """With the MFMA heads kernel a board's outputs depend only on its planes, bit for bit
+        whatever batch it is in (tests/test_gpu_tower.py): duplicate leaves of a batch may share one
+        row (SelfPlayEngine leaf_dedup).  The torch-GEMM heads are not batch-independent."""
+        return self.fused_heads is True
+
     leaf_format = "bf16"
     leaf_layout = "nhwc"
     bucket = 1  # the HIP kernels take any batch size; no shape padding needed
