@@ -11,6 +11,7 @@ LANES=2 PSTEPS=3 bash scripts/gpu_prof_bench.sh
 rc=$?; if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -s KILL 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_MFMA \
   --kernel-include-regex "k_tower_dyn" -f csv -d gpurun_out/util/bench -o run -- \
-  python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/util/bench_pmc.json 2> gpurun_out/util/bench_pmc.err
+  python3 bench.py --steps 2 --warmup 24 --no-cpu-baseline > gpurun_out/util/bench_pmc.json 2> gpurun_out/util/bench_pmc.err
 rc=$?; echo "clock pmc rc=$rc"; if [ $rc -ne 0 ]; then tail -5 gpurun_out/util/bench_pmc.err; exit $rc; fi
-python3 scripts/tower_util.py gpurun_out/util/bench/run_counter_collection.csv gpurun_out/util/tower_util_bench.json
+python3 scripts/tower_util.py gpurun_out/util/bench/run_counter_collection.csv gpurun_out/util/tower_util_bench.json \
+  $(python3 -c "import json; d=json.loads([l for l in open('gpurun_out/util/bench_pmc.json') if l.startswith('{')][0]); print(d['roofline']['dispatches'])")

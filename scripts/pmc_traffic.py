@@ -9,16 +9,24 @@ import json
 import sys
 
 
-def mean_counter(path, name, kernel="k_tower_dyn"):
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-            if kernel in r["Kernel_Name"] and r["Counter_Name"] == name]
+def mean_counter(path, name, kernel="k_tower_dyn", last=0):
+    """Mean per dispatch (counter rows summed per dispatch); `last` > 0 keeps the last N dispatches
+    (the bench's timed region, after its warm-up plies)."""
+    per = {}
+    for r in csv.DictReader(open(path)):
+        if kernel in r["Kernel_Name"] and r["Counter_Name"] == name:
+            d = int(r["Dispatch_Id"])
+            per[d] = per.get(d, 0.0) + float(r["Counter_Value"])
+    vals = [per[d] for d in sorted(per)]
+    if last > 0:
+        vals = vals[-last:]
     return sum(vals) / len(vals), len(vals)
 
 
-def main(fetch_csv, write_csv, out_json, lanes="1"):
-    lanes = int(lanes)
-    fetch, n = mean_counter(fetch_csv, "FETCH_SIZE")
-    write, _ = mean_counter(write_csv, "WRITE_SIZE")
+def main(fetch_csv, write_csv, out_json, lanes="1", last="0"):
+    lanes, last = int(lanes), int(last)
+    fetch, n = mean_counter(fetch_csv, "FETCH_SIZE", last=last)
+    write, _ = mean_counter(write_csv, "WRITE_SIZE", last=last)
     per_dispatch = 2 * fetch * 1024 + write * 1024
     res = dict(kernel="k_tower_dyn", dispatches=n, lanes=lanes, fetch_kib=fetch, write_kib=write,
                read_bytes=2 * fetch * 1024, write_bytes=write * 1024,
@@ -32,4 +40,4 @@ def main(fetch_csv, write_csv, out_json, lanes="1"):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:5])
+    main(*sys.argv[1:6])

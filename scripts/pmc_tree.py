@@ -9,20 +9,30 @@ import sys
 KERNELS = ("k_select_vl", "k_expand_vl")
 
 
-def per_kernel(path, name):
-    out = {k: [] for k in KERNELS}
+def per_kernel(path, name, last=0):
+    """Counter per dispatch of each tree kernel; `last` > 0 keeps the last N tree dispatches (both
+    kernels together, dispatch order: the bench's timed region)."""
+    per = {}
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != name:
             continue
         for k in KERNELS:
             if k in r["Kernel_Name"]:
-                out[k].append(float(r["Counter_Value"]))
+                d = int(r["Dispatch_Id"])
+                kk, v = per.get(d, (k, 0.0))
+                per[d] = (k, v + float(r["Counter_Value"]))
+    ids = sorted(per)
+    if last > 0:
+        ids = ids[-last:]
+    out = {k: [] for k in KERNELS}
+    for d in ids:
+        out[per[d][0]].append(per[d][1])
     return out
 
 
-def main(fetch_csv, write_csv, out_json):
-    f = per_kernel(fetch_csv, "FETCH_SIZE")
-    w = per_kernel(write_csv, "WRITE_SIZE")
+def main(fetch_csv, write_csv, out_json, last="0"):
+    f = per_kernel(fetch_csv, "FETCH_SIZE", int(last))
+    w = per_kernel(write_csv, "WRITE_SIZE", int(last))
     res = dict(kernels={})
     tot_bytes, tot_n = 0.0, 0
     for k in KERNELS:
@@ -43,4 +53,4 @@ def main(fetch_csv, write_csv, out_json):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])

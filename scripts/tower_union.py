@@ -4,17 +4,21 @@ With L lanes (bench.py --lanes, engine.LanedEngine) the L k_tower_dyn dispatches
 step run concurrently, so bench.py reports roofline.avg_launch_us = union busy time of all
 k_tower_dyn dispatches / (dispatches / L).  This recomputes the same figure from rocprof's own
 start/end timestamps, beside rocprof's per-dispatch average (= bench.py's avg_dispatch_us).
-The traced run includes its warmup plies, so both are averages over every dispatch of the run.
+`last` (optional): keep only the last N dispatches (the bench's timed region: bench.py reports its
+roofline.dispatches), so warm-up plies - with leaf dedup, early plies have far fewer rows - do not
+enter the averages.
 """
 import csv
 import json
 import sys
 
 
-def main(trace_csv, lanes, out_json, kernel="k_tower_dyn"):
-    lanes = int(lanes)
+def main(trace_csv, lanes, out_json, last=0, kernel="k_tower_dyn"):
+    lanes, last = int(lanes), int(last)
     iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(open(trace_csv))
                 if kernel in r["Kernel_Name"])
+    if last > 0:
+        iv = iv[-last:]
     busy, cs, ce = 0, None, None
     for a, b in iv:
         if ce is None or a > ce:
@@ -37,4 +41,4 @@ def main(trace_csv, lanes, out_json, kernel="k_tower_dyn"):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])

@@ -1105,9 +1105,28 @@ __global__ __launch_bounds__(64) void k_expand(View v, const float *probs0, cons
 // earlier slots of the same tree have changed the shared ancestors.  Pending leaves of trees that
 // are not searching (a _set_node expansion, slot 0, path length 0) are completed without a refill.
 // ----------------------------------------------------------------------------
+template <class G, int TB>
+__device__ __forceinline__ void expand_vl_body(View v, const float *probs0, const float *values0,
+                                               const float *probs1, const float *values1);
+
 template <class G, int TB = 64>
 __global__ __launch_bounds__(TB) void k_expand_vl(View v, const float *probs0, const float *values0,
                                                   const float *probs1, const float *values1) {
+  expand_vl_body<G, TB>(v, probs0, values0, probs1, values1);
+}
+
+// The same held to 96 registers (SPMCTS_EXPAND_CO=1, a timing variant): its waves then fit on a SIMD
+// beside a trunk wave (416 registers) instead of waiting for the trunk workgroup to retire, at the
+// price of register spills on the dependent chain.
+template <class G>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_expand_vl_co(
+    View v, const float *probs0, const float *values0, const float *probs1, const float *values1) {
+  expand_vl_body<G, 64>(v, probs0, values0, probs1, values1);
+}
+
+template <class G, int TB>
+__device__ __forceinline__ void expand_vl_body(View v, const float *probs0, const float *values0,
+                                               const float *probs1, const float *values1) {
   constexpr int P = G::APAD;
   constexpr int GPB = TB / P;
   constexpr int KMAX = P;  // slots whose records one lane each prefetches (spmcts_arena_create: K <= P)
@@ -2152,7 +2171,15 @@ int spmcts_expand2(spmcts_arena *h, const float *probs0_dev, const float *values
   const int gpb = 64 / h->P;
   if (h->v.K > 1) {
     const int tb = h->tree_block, tpb = tb / h->P;
-    if (tb > 64)
+    static int co = -1;
+    if (co < 0) {
+      const char *e = getenv("SPMCTS_EXPAND_CO");
+      co = e && atoi(e) ? 1 : 0;
+    }
+    if (co && tb == 64)
+      DISPATCH(h, hipLaunchKernelGGL(k_expand_vl_co<GG>, dim3(nblk(h->v.T, tpb)), dim3(tb), 0, (hipStream_t)stream,
+                                     h->v, probs0_dev, values0_dev, probs1_dev, values1_dev));
+    else if (tb > 64)
       DISPATCH(h, hipLaunchKernelGGL((k_expand_vl<GG, 512>), dim3(nblk(h->v.T, tpb)), dim3(tb), 0, (hipStream_t)stream,
                                      h->v, probs0_dev, values0_dev, probs1_dev, values1_dev));
     else
