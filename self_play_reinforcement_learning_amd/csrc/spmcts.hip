@@ -124,6 +124,7 @@ struct View {
   // one row.  dtab: open-addressing table of (generation << 32 | owner slot), dent: a slot's entry
   uint64_t *dtab;
   int32_t *dent;
+  uint8_t *down;  // 1 = the slot owns its key's row (set per step by k_dedup_owner)
   int dedup, dmask;
   uint32_t dgen;
   float *root_prior;
@@ -939,9 +940,15 @@ __global__ __launch_bounds__(256) void k_dedup_insert(View v) {
   set_err(v, SPMCTS_ERR_STATE);  // unreachable: the table has >= 2 NS entries
 }
 
-__device__ __forceinline__ bool row_owner(const View &v, int t) {
-  return v.need[t] && (!v.dedup || (int)(uint32_t)v.dtab[v.dent[t]] == t);
+// owner flags, one independent load pair per slot (the scan below then reads one byte per slot
+// instead of a dependent dent -> dtab chain per slot in its serial chunk loop)
+__global__ __launch_bounds__(256) void k_dedup_owner(View v) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= v.NS) return;
+  v.down[t] = v.need[t] && (int)(uint32_t)v.dtab[v.dent[t]] == t ? 1 : 0;
 }
+
+__device__ __forceinline__ bool row_owner(const View &v, int t) { return v.dedup ? v.down[t] != 0 : v.need[t] != 0; }
 
 // duplicates read their owner's row
 __global__ __launch_bounds__(256) void k_dedup_alias(View v) {
@@ -958,6 +965,8 @@ __global__ __launch_bounds__(1024) void k_scan_need(View v, int32_t *count_out) 
   const int chunk = (T + 1023) / 1024;
   const int lo = min(T, tid * chunk), hi = min(T, lo + chunk);
   int c0 = 0, c1 = 0;
+  // unrolled so each thread's chunk of flags is fetched in one round of independent loads
+#pragma unroll 16
   for (int t = lo; t < hi; ++t)
     if (row_owner(v, t)) {
       if (v.tnet[t / v.K]) ++c1; else ++c0;
@@ -975,6 +984,7 @@ __global__ __launch_bounds__(1024) void k_scan_need(View v, int32_t *count_out) 
     __syncthreads();
   }
   int r0 = s_p0[tid] - c0, r1 = v.seg1 + s_p1[tid] - c1;
+#pragma unroll 16
   for (int t = lo; t < hi; ++t)
     if (row_owner(v, t)) {
       const int r = v.tnet[t / v.K] ? r1++ : r0++;
@@ -1849,6 +1859,7 @@ static void plan_arena(spmcts_arena *h, Plan &pl) {
     v.dmask = (int)(tab - 1);
     pl.add(&v.dtab, v.K > 1 ? tab : 1);
     pl.add(&v.dent, v.K > 1 ? NS : 1);
+    pl.add(&v.down, v.K > 1 ? NS : 1);
   }
   pl.add(&v.root_prior, 32);  // [net][16]
   pl.add(&v.err, 4);
@@ -2120,6 +2131,7 @@ static int launch_rows(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_de
   if (h->v.dedup) {
     if (++h->v.dgen == 0) ++h->v.dgen;  // generation 0 = the zeroed table
     DISPATCH(h, hipLaunchKernelGGL(k_dedup_insert<GG>, dim3(nblk(h->v.NS, 256)), dim3(256), 0, s, h->v));
+    hipLaunchKernelGGL(k_dedup_owner, dim3(nblk(h->v.NS, 256)), dim3(256), 0, s, h->v);
   }
   hipLaunchKernelGGL(k_scan_need, dim3(1), dim3(1024), 0, s, h->v, leaf_count_dev);
   if (h->v.dedup) hipLaunchKernelGGL(k_dedup_alias, dim3(nblk(h->v.NS, 256)), dim3(256), 0, s, h->v);
