@@ -13,7 +13,11 @@ on each rank's device and, once per episode batch (--exchange-every plies), the
 episode statistics are all-reduced and the records gathered to rank 0 (the
 replay owner), as in the north star.  Each GPU's games are held in
 --lanes arenas (default 2, engine.LanedEngine) on their own HIP streams, so one
-arena's tree kernels run beside the other's ResNet launch.
+arena's tree kernels run beside the other's ResNet launch.  Pending leaves of a
+simulation step that are the same network input share one evaluation (batch
+leaf dedup, default; --no-leaf-dedup evaluates every leaf in its own row as the
+reference's InferenceWorker does): the searches are bit-identical either way
+(tests/test_gpu_engine.py), and the line reports nn.rows beside nn.leaves.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
