@@ -100,6 +100,40 @@ __host__ __device__ __forceinline__ double philox_uniform_at(PhiloxFields f, uns
   return rocrand_device::detail::uniform_distribution_double(v1, v2);
 }
 
+// The same draws for a whole group of lanes at once: lane j's words sit at positions sub + 2j and
+// sub + 2j + 1 past the state's block, i.e. in output blocks (sub + 2j) >> 2 and the next one, so the
+// group computes each block once (lane b: block b) and every lane picks its words from the lane that
+// holds them, instead of every lane computing two blocks.  Host-testable pieces:
+__host__ __device__ __forceinline__ void philox_group_src(unsigned int sub, int j, int &blk, unsigned int &w) {
+  const unsigned int p = sub + 2u * (unsigned int)j;
+  blk = (int)(p >> 2);
+  w = p & 3u;
+}
+
+// the draw from block `b` (word w, and w + 1 or the next block's first word)
+__host__ __device__ __forceinline__ double philox_group_value(uint4 b, unsigned int next_x, unsigned int w) {
+  const unsigned int v1 = philox_word(b, w);
+  const unsigned int v2 = w < 3u ? philox_word(b, w + 1u) : next_x;
+  return rocrand_device::detail::uniform_distribution_double(v1, v2);
+}
+
+// Device form: every lane of the P-lane group (gbase = its first lane in the wave) must call it;
+// lane j's result equals philox_uniform_at(f, 2j).  Blocks up to (3 + 2P) / 4 + 1 < P are needed.
+template <int P>
+__device__ __forceinline__ double philox_uniform_group(const PhiloxFields &f, int j, int gbase) {
+  static_assert((3 + 2 * P) / 4 + 1 < P, "the group holds every block its draws touch");
+  const uint4 mine = philox10(philox_add(f.counter, (unsigned long long)j), f.key);  // block j
+  int blk;
+  unsigned int w;
+  philox_group_src(f.substate, j, blk, w);
+  const int src = gbase + (blk < P ? blk : P - 1);
+  const int nxt = gbase + (blk + 1 < P ? blk + 1 : P - 1);
+  const uint4 b = uint4{(unsigned int)__shfl((int)mine.x, src, 64), (unsigned int)__shfl((int)mine.y, src, 64),
+                        (unsigned int)__shfl((int)mine.z, src, 64), (unsigned int)__shfl((int)mine.w, src, 64)};
+  const unsigned int nx = (unsigned int)__shfl((int)mine.x, nxt, 64);
+  return philox_group_value(b, nx, w);
+}
+
 // restore rocRAND's invariant result == philox10(counter) before the state is stored or handed to
 // rocRAND's own functions
 __host__ __device__ __forceinline__ void philox_sync(PhiloxFields &f) { f.result = philox10(f.counter, f.key); }

@@ -221,6 +221,15 @@ __device__ __forceinline__ void rng_advance(const View &v, TreeRng &r, int k) {
     philox_skip(r.f, 2ull * (unsigned long long)k);  // skipahead(2k) minus its output-block refresh
 }
 
+// Child jitter of a P-lane tree group, lane j < A using its draw (= rng_lane(j)); every lane of the
+// group must call it.  Tape mode reads lane j's tape entry; Philox mode computes each output block
+// once per group and shares it through shuffles (philox.h philox_uniform_group).
+template <class G>
+__device__ __forceinline__ double rng_group(const View &v, const TreeRng &r, int lane, int gbase, bool *tape_err) {
+  if (v.rng_mode == SPMCTS_RNG_TAPE) return lane < G::A ? rng_lane(v, r, lane, tape_err) : 0.0;
+  return 1.0 - philox_uniform_group<G::APAD>(r.f, lane, gbase);
+}
+
 // sequential scalar draw (single thread)
 __device__ __forceinline__ double rng_next(const View &v, TreeRng &r, bool *tape_err) {
   double u = rng_lane(v, r, 0, tape_err);
@@ -571,6 +580,10 @@ __global__ __launch_bounds__(64) void k_select(View v, int n_active) {
       cp = v.bp[ci];
       cc = v.bc[ci];
     }
+    const int gbase = (threadIdx.x & 63) & ~(P - 1);
+    // the jitter does not depend on the child block: drawn here, it overlaps the loads above
+    bool terr_j = false;
+    const double jit = rng_group<G>(v, rng, lane, gbase, &terr_j);
     const bool valid = (lane < G::A) && ((vm >> lane) & 1u);
     double score = -10000000000.0;  // mcts.py:347
     if (valid) {
@@ -588,12 +601,12 @@ __global__ __launch_bounds__(64) void k_select(View v, int n_active) {
       return;
     }
     // argmax(select_probs + 1e-6 * rand(A)) (mcts.py:355): first index on ties
+    terr = terr || terr_j;
     double s = -INFINITY;
-    if (lane < G::A) s = score + 0.000001 * rng_lane(v, rng, lane, &terr);
+    if (lane < G::A) s = score + 0.000001 * jit;
     rng_advance(v, rng, G::A);
     int a = lane;
     group_argmax<P>(s, a);
-    const int gbase = (threadIdx.x & 63) & ~(P - 1);
     const int cc_a = __shfl(cc, gbase + a, 64);
     const int cn_a = __shfl(cn, gbase + a, 64);
     const double cw_a = __shfl(cw, gbase + a, 64);
@@ -743,6 +756,9 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
       cc = v.bc[ci];
       cvl = v.bvl[ci];
     }
+    // the jitter does not depend on the child block: drawn here, it overlaps the loads above
+    bool terr_j = false;
+    const double jit = rng_group<G>(v, rng, lane, gbase, &terr_j);
     // valid (mcts.py:86-88): valid move and not locked by a pending sim
     const bool valid = (lane < G::A) && ((vm >> lane) & 1u) && cc != -2;
     double score = -10000000000.0;
@@ -759,8 +775,9 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
       if (lane == 0) cnt[C_LEAK] += 1;
       return SIM_LEAK;
     }
+    terr = terr || terr_j;  // (a leak consumes no draw, so its tape check does not count)
     double s = -INFINITY;
-    if (lane < G::A) s = score + 0.000001 * rng_lane(v, rng, lane, &terr);
+    if (lane < G::A) s = score + 0.000001 * jit;
     rng_advance(v, rng, G::A);
     int a = lane;
     group_argmax<P>(s, a);

@@ -37,6 +37,24 @@ int main() {
         ++bad;
       }
     }
+    // the group form's index math: lane j's draw from the blocks b = 0, 1, ... (block b = counter + b)
+    {
+      const PhiloxFields f = philox_fields(s);
+      uint4 blocks[12];
+      for (int b = 0; b < 12; ++b) blocks[b] = philox10(philox_add(f.counter, (unsigned long long)b), f.key);
+      for (int j = 0; j < 16; ++j) {
+        int blk;
+        unsigned int w;
+        philox_group_src(f.substate, j, blk, w);
+        const double got = philox_group_value(blocks[blk], blocks[blk + 1].x, w);
+        const double want = philox_uniform_at(f, 2ull * j);
+        ++checks;
+        if (memcmp(&want, &got, sizeof want) != 0) {
+          if (bad < 5) printf("group draw mismatch it=%d j=%d\n", it, j);
+          ++bad;
+        }
+      }
+    }
     for (int k = 1; k <= 16; k += 3) {
       rocrand_state_philox4x32_10 a = s;
       skipahead(2ull * k, &a);
