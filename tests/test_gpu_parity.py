@@ -339,3 +339,21 @@ def test_threaded_evaluation_games_match_oracle(key):
             assert moves["tree_probs"][i].astype(float).tolist() == M["tree_probs"].astype(float).tolist(), (gi, i)
             q = np.float64(moves["q"][i]) if moves["q_f64"][i] else np.float32(moves["q"][i])
             assert float(q) == float(M["q"]), (gi, i)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tree_block", [512, 8])
+def test_threaded_search_tree_workgroups(tree_block, monkeypatch):
+    """The threaded tree kernels give the same searches with 8 trees per 64-thread workgroup (the
+    default), 64 trees per 512-thread workgroup, or one tree per workgroup (SPMCTS_TREE_BLOCK, read
+    when an arena is created)."""
+    from tests.parity_helpers import g2_threaded
+
+    monkeypatch.setenv("SPMCTS_TREE_BLOCK", str(tree_block))
+    key, cases = _threaded_groups()[0]
+    runs = [g2_threaded(c, 4) for c in cases]
+    res, counters = run_g2_group(cases, search_threads=4, tapes=[t for t, _ in runs])
+    assert counters["error_flags"] == 0
+    for c, (_, e), r in zip(cases, runs, res):
+        assert r["child_n"] == e["child_n"] and r["child_w"] == e["child_w"], c["id"]
+        assert r["action"] == e["action"], c["id"]
