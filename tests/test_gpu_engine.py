@@ -399,11 +399,13 @@ def _run_moves(eng, games):
     return {k: np.concatenate([g[k] for g in got]) for k in got[0]}, eng.counters()
 
 
-@pytest.mark.parametrize("game,n_games,sims", [("connect4", 512, 16), ("tictactoe", 256, 24)])
-def test_leaf_dedup_is_exact(game, n_games, sims):
+@pytest.mark.parametrize("game,n_games,sims,bpt", [("connect4", 512, 16, 0), ("tictactoe", 256, 24, 0),
+                                                   ("connect4", 256, 16, 6 * 16 + 64)])
+def test_leaf_dedup_is_exact(game, n_games, sims, bpt):
     """Batch leaf dedup (one row per distinct network input of a simulation step) changes nothing
     a search sees: the same Move records bit for bit and the same counters, with fewer network rows
-    (games start from the empty board, so early steps are mostly duplicates)."""
+    (games start from the empty board, so early steps are mostly duplicates); also beside subtree
+    recycling (bpt > 0: a node store of 6 searches' worth of blocks)."""
     from self_play_reinforcement_learning_amd.engine import SelfPlayEngine
     from self_play_reinforcement_learning_amd.modules import ResidualTower
 
@@ -413,7 +415,7 @@ def test_leaf_dedup_is_exact(game, n_games, sims):
     out = []
     for dedup in (False, True):
         eng = SelfPlayEngine(game, net, n_games=n_games, iterations=sims, seed=3, max_games=2 * n_games,
-                             search_threads=4, leaf_dedup=dedup)
+                             search_threads=4, leaf_dedup=dedup, blocks_per_tree=bpt)
         assert eng.leaf_dedup == dedup and eng.evaluator.pure_planes
         out.append(_run_moves(eng, 2 * n_games))
     (m0, c0), (m1, c1) = out
@@ -424,6 +426,7 @@ def test_leaf_dedup_is_exact(game, n_games, sims):
         assert c0[k] == c1[k], k
     assert c0["nn_rows"] == c0["nn_leaves"]
     assert c1["nn_rows"] < c1["nn_leaves"]
+    assert (c1["compactions"] > 0) == (bpt > 0)  # with a small store: dedup beside subtree recycling
 
 
 def test_leaf_dedup_two_networks_exact():
