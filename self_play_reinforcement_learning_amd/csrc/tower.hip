@@ -151,6 +151,7 @@ struct Nbr {
   int rowi[K::NT];
   uint32_t mask[K::NT];
   const uint16_t *tab;  // Cfg::EDGE: LDS neighbour-row table [9][ROWS]
+  int off0[K::NT];      // tap 0's operand offsets (the same for every layer; set by finish())
   __device__ __forceinline__ void init(int r, int mg) {
 #pragma unroll
     for (int t = 0; t < K::NT; ++t) {
@@ -169,6 +170,14 @@ struct Nbr {
       mask[t] = m;
     }
   }
+  // once the table is in LDS: tap 0's offsets, kept for every layer's first operand reads (a table
+  // read there would stall each layer start on an LDS round trip)
+  __device__ __forceinline__ void finish() {
+#pragma unroll
+    for (int t = 0; t < K::NT; ++t) off0[t] = off(t, 0);
+  }
+  // Cfg::EDGE: the source row of tile t for `tap` (an LDS table read; times RS = off())
+  __device__ __forceinline__ int row(int t, int tap) const { return (int)tab[tap * K::ROWS + rowi[t]]; }
   // byte offset of the source row of tile t for `tap` (the zero row when off the board); a
   // branch-free select (hipcc otherwise emits an exec-mask branch per tile and tap)
   __device__ __forceinline__ int off(int t, int tap) const {
@@ -570,9 +579,13 @@ __device__ __forceinline__ void conv_tap_x(const char *src, const Nbr<K> &nb, f3
   constexpr int NTA = (int)X::popc(LV);
   static_assert(NTA >= 1 && K::MT * NTA >= NTA + K::MT, "schedule: enough MFMAs for the loads");
   if constexpr (TAP < 8) {
+    // the next tap's neighbour rows are read here, ahead of this tap's operand reads, and turned
+    // into addresses only where the tap's last k-step uses them: read at the tap boundary they made
+    // the wave drain its whole LDS queue there (s_waitcnt lgkmcnt(0)), 8 times a layer
 #pragma unroll
     for (int t = 0; t < K::NT; ++t)
-      if ((LVN >> t) & 1u) off_nxt[t] = nb.off(t, TAP + 1) + hoff;
+      if ((LVN >> t) & 1u) off_nxt[t] = nb.row(t, TAP + 1);
+    __builtin_amdgcn_sched_barrier(0);
   }
 #pragma unroll
   for (int kk = 0; kk < KK; ++kk) {
@@ -587,7 +600,10 @@ __device__ __forceinline__ void conv_tap_x(const char *src, const Nbr<K> &nb, f3
     } else if (TAP < 8) {
 #pragma unroll
       for (int t = 0; t < K::NT; ++t)
-        if ((LVN >> t) & 1u) bn[t] = lds_b128(src + off_nxt[t]);
+        if ((LVN >> t) & 1u) {
+          off_nxt[t] = off_nxt[t] * K::RS + hoff;  // row -> byte offset (see the top of the tap)
+          bn[t] = lds_b128(src + off_nxt[t]);
+        }
     }
     const int slot = kk % DEPTH;
     bf16x8 acur[K::MT];
@@ -748,7 +764,7 @@ __device__ __forceinline__ void conv_layer_x(const char *src, char *dst, const N
 #pragma unroll
   for (int t = 0; t < K::NT; ++t)
     if (((K::EDGE ? X::lt(0) : X::LIVE[0]) >> t) & 1u) {
-      off_cur[t] = nb.off(t, 0) + hoff;
+      off_cur[t] = nb.off0[t] + hoff;
       bc[t] = lds_b128(src + off_cur[t]);
     }
   if constexpr (K::EDGE) {
@@ -883,6 +899,7 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
     for (int c = 0; c < 16; ++c) dst[c] = (ok && c < 3) ? planes[src + c] : (__bf16)0.f;
   }
   __syncthreads();
+  nb.finish();
 
   constexpr int KK = K::C / 16;
   constexpr int DEPTH = K::DEPTH;
