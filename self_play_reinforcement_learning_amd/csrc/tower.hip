@@ -29,9 +29,9 @@
 
 namespace tower {
 
-// edge-tile layout tables (tower_edge.h): row -> (board, x, y) packed, (board, x, y) -> row
+// edge-tile layout tables (tower_edge.h): row -> (board, x, y) packed (the inverse map,
+// EDGE_CELL_ROW_INIT, is used only by the host-side layout tests)
 constexpr uint16_t kEdgeRow[256] = EDGE_ROW_INIT;
-constexpr uint16_t kEdgeCellRow[6 * 7 * 6] = EDGE_CELL_ROW_INIT;
 // [tap][row] source row (zero rows off the board, at bank positions no on-board lane of the
 // 16-lane read group uses)
 constexpr uint16_t kEdgeNbr[9 * 256] = EDGE_NBR_INIT;
@@ -357,7 +357,6 @@ __device__ __forceinline__ void acc_store_relu(const f32x16 (&acc)[K::MT][K::NT]
   for (int m = 0; m < K::MT; ++m)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const int ch = ((wave % K::CG) * K::MT + m) * 32 + 8 * g + 4 * h;
 #pragma unroll
       for (int t = 0; t < K::NT; ++t) {
         bf16x4 o;
