@@ -1,7 +1,7 @@
 # The bench's multi-rank path on RCCL (backend "nccl") with 2 ranks sharing the box's one GPU, short
 # and under its own time limit: checks the exchange rounds, barrier and max-over-ranks timing on the
-# collective library the driver's 8-GPU run uses.  RCCL may refuse two ranks on one device; the log
-# says so and nothing else runs.
+# collective library the driver's 8-GPU run uses.  Measured: RCCL refuses two ranks on one device
+# ("Duplicate GPU detected", profiles/r02/rccl_2rank_one_gpu.txt); kept for multi-GPU boxes.
 set -u
 mkdir -p gpurun_out/nccl
 export TMPDIR=/tmp SPMCTS_DIST_BACKEND=nccl NCCL_DEBUG=WARN
