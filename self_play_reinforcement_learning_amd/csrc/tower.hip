@@ -29,6 +29,15 @@
 
 namespace tower {
 
+// The weight ring's loads for the next layer's first DEPTH k-steps are issued unconditionally (the
+// last conv re-reads its own first steps, discarded): a conditional load made hipcc merge the ring
+// registers with copies at every layer's last k-step, behind an s_waitcnt vmcnt(0) that drained
+// the whole weight pipeline once per layer.
+#ifndef SPMCTS_RING_ALWAYS
+#define SPMCTS_RING_ALWAYS 1
+#endif
+constexpr bool kRingAlways = SPMCTS_RING_ALWAYS != 0;
+
 // edge-tile layout tables (tower_edge.h): row -> (board, x, y) packed (the inverse map,
 // EDGE_CELL_ROW_INIT, is used only by the host-side layout tests)
 constexpr uint16_t kEdgeRow[256] = EDGE_ROW_INIT;
@@ -447,7 +456,7 @@ __device__ __forceinline__ void conv_layer(const char *src, char *dst, const Nbr
         if (sn < STEPS) {
 #pragma unroll
           for (int m = 0; m < K::MT; ++m) a[slot][m] = wb.load(wl_off + m * MSTRIDE + (uint32_t)sn * 1024u);
-        } else if (sn - STEPS < wn_steps) {
+        } else if (kRingAlways || sn - STEPS < wn_steps) {
 #pragma unroll
           for (int m = 0; m < K::MT; ++m)
             a[slot][m] = wb.load(wn_off + m * MSTRIDE + (uint32_t)(sn - STEPS) * 1024u);
@@ -455,7 +464,7 @@ __device__ __forceinline__ void conv_layer(const char *src, char *dst, const Nbr
       } else if (sn < STEPS) {
 #pragma unroll
         for (int m = 0; m < K::MT; ++m) a[slot][m] = wl[m][(size_t)sn * 64];
-      } else if (sn - STEPS < wn_steps) {
+      } else if (sn - STEPS < wn_steps) {  // (pointer-path ablation: wn is past the convs after the last)
 #pragma unroll
         for (int m = 0; m < K::MT; ++m) a[slot][m] = wn[m][(size_t)(sn - STEPS) * 64];
       }
@@ -619,7 +628,7 @@ __device__ __forceinline__ void conv_tap_x(const char *src, const Nbr<K> &nb, f3
     } else if (sn < STEPS) {
 #pragma unroll
       for (int m = 0; m < K::MT; ++m) a[slot][m] = wb.template load<WAUX>(wl_off + m * MSTRIDE + (uint32_t)sn * 1024u);
-    } else if (sn - STEPS < wn_steps) {
+    } else if (kRingAlways || sn - STEPS < wn_steps) {
 #pragma unroll
       for (int m = 0; m < K::MT; ++m)
         a[slot][m] = wb.template load<WAUX>(wn_off + m * MSTRIDE + (uint32_t)(sn - STEPS) * 1024u);
@@ -699,7 +708,7 @@ __device__ __forceinline__ void conv_group_x(const char *src, const Nbr<K> &nb, 
       if (sn < STEPS) {
 #pragma unroll
         for (int m = 0; m < K::MT; ++m) a[slot][m] = wb.load(wl_off + m * MSTRIDE + (uint32_t)sn * 1024u);
-      } else if (sn - STEPS < wn_steps) {
+      } else if (kRingAlways || sn - STEPS < wn_steps) {
 #pragma unroll
         for (int m = 0; m < K::MT; ++m) a[slot][m] = wb.load(wn_off + m * MSTRIDE + (uint32_t)(sn - STEPS) * 1024u);
       }
@@ -926,7 +935,7 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
   const uint32_t ct0_off = (uint32_t)(STEM + (size_t)((wave_u % K::CG) * K::MT) * LSTEPS * 64) * 16u;
   for (int L = 0; L < n_convs; ++L) {
     const uint32_t wl_off = ct0_off + (uint32_t)((size_t)L * LAYER * 16u);
-    const uint32_t wn_off = wl_off + (uint32_t)(LAYER * 16u);
+    const uint32_t wn_off = (kRingAlways && L + 1 == n_convs) ? wl_off : wl_off + (uint32_t)(LAYER * 16u);
     const bf16x8 *wl[K::MT], *wn[K::MT];
 #pragma unroll
     for (int m = 0; m < K::MT; ++m) {
