@@ -839,6 +839,10 @@ __device__ __forceinline__ void head_layer(const char *src, const bf16x8 *w, con
   bf16x8 wf[KK];
 #pragma unroll
   for (int kk = 0; kk < KK; ++kk) wf[kk] = w[((size_t)ct * KK + kk) * 64 + lane];
+  // the epilogue's bias too (fetched inside the store loop, each fetch waited behind the stores)
+  float4 bvs[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) bvs[g] = *(const float4 *)(bias + ct * 32 + 8 * g + 4 * h);
 #pragma unroll
   for (int kk = 0; kk < KK; ++kk) {
     const bf16x8 a = wf[kk];
@@ -850,23 +854,31 @@ __device__ __forceinline__ void head_layer(const char *src, const bf16x8 *w, con
       acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[t], 0, 0, 0);
     }
   }
+  // each lane's output rows, looked up once per cell tile (the row -> board/cell table is read from
+  // global memory: looked up inside the store loop, every lookup waited for its own load)
+  size_t obase[TPW];
+  bool okr[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int row = (t0 + t) * 32 + r;
+    const int rr = row < K::VROWS ? row : 0;
+    const int board = board0 + K::row_board(rr);
+    okr[t] = row < K::VROWS && board < batch;
+    obase[t] = ((size_t)board * K::CELLS + K::row_cell(rr)) * K::HEAD;
+  }
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int ch = ct * 32 + 8 * g + 4 * h;
-    const float4 bv = *(const float4 *)(bias + ch);
+    const float4 bv = bvs[g];
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
-      const int row = (t0 + t) * 32 + r;
-      if (row >= K::VROWS) continue;
-      const int board = board0 + K::row_board(row);
-      if (board >= batch) continue;
-      const int cell = K::row_cell(row);
+      if (!okr[t]) continue;
       bf16x4 o;
       o[0] = (__bf16)fmaxf(acc[t][4 * g + 0] + bv.x, 0.f);
       o[1] = (__bf16)fmaxf(acc[t][4 * g + 1] + bv.y, 0.f);
       o[2] = (__bf16)fmaxf(acc[t][4 * g + 2] + bv.z, 0.f);
       o[3] = (__bf16)fmaxf(acc[t][4 * g + 3] + bv.w, 0.f);
-      *(bf16x4 *)(out + ((size_t)board * K::CELLS + cell) * K::HEAD + ch) = o;
+      *(bf16x4 *)(out + obase[t] + ch) = o;
     }
   }
 }
@@ -895,7 +907,10 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
   if constexpr (K::EDGE) {
     uint16_t *tab = (uint16_t *)(smem + 2 * K::BUF);
     static_assert(K::ROWS == 256 && K::ZROW == 256, "EDGE_NBR is laid out for 256-row tiles");
-    for (int i = tid; i < 9 * K::ROWS; i += K::THREADS) tab[i] = kEdgeNbr[i];
+    static_assert(9 * K::ROWS % K::THREADS == 0, "neighbour table copy: whole rounds");
+    // unrolled so all of a thread's table loads are in flight at once (a rolled loop waited for each)
+#pragma unroll
+    for (int j = 0; j < 9 * K::ROWS / K::THREADS; ++j) tab[tid + j * K::THREADS] = kEdgeNbr[tid + j * K::THREADS];
     nb.tab = tab;
   }
   for (int row = tid; row < K::ROWS; row += K::THREADS) {
