@@ -7,8 +7,9 @@ L=$PWD/self_play_reinforcement_learning_amd
 set -- $LIBS
 A=$1; B=$2
 SPMCTS_LIB=$L/$A timeout -k 10 180 python3 scripts/tower_code_equal.py dump gpurun_out/lt/a.npz && \
-SPMCTS_LIB=$L/$B timeout -k 10 180 python3 scripts/tower_code_equal.py dump gpurun_out/lt/b.npz && \
-python3 scripts/tower_code_equal.py cmp gpurun_out/lt/a.npz gpurun_out/lt/b.npz || exit 1
+SPMCTS_LIB=$L/$B timeout -k 10 180 python3 scripts/tower_code_equal.py dump gpurun_out/lt/b.npz || exit 1
+# NOEQ=1: a numerics change (the tower tests below are then the check); the comparison is printed
+python3 scripts/tower_code_equal.py cmp gpurun_out/lt/a.npz gpurun_out/lt/b.npz || [ "${NOEQ:-0}" = 1 ] || exit 1
 SPMCTS_LIB=$L/$B timeout -k 10 300 python -u -m pytest tests/test_gpu_tower.py -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/lt/tests.log 2>&1
 rc=$?; tail -1 gpurun_out/lt/tests.log; if [ $rc -ne 0 ]; then exit $rc; fi
 for BATCH in 1536 6144; do
