@@ -21,7 +21,10 @@ reference's InferenceWorker does): the searches are bit-identical either way
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
-Prints ONE JSON line on rank 0.
+Prints ONE JSON line on rank 0.  Without torchrun, --gpus N > 1 starts the N rank processes itself
+(before this process touches the GPU) with torchrun's environment, one per GPU; it refuses N ranks
+on fewer visible GPUs unless SPMCTS_ALLOW_OVERSUBSCRIBE=1 (a rehearsal; with SPMCTS_DIST_BACKEND=gloo,
+since RCCL refuses two ranks on one GPU).
 
 Secondary workloads (BASELINE.json configs; not the headline line):
   --sims 800 --games 16384 --filter-factor 64   config 3 (deep trees, ResNet-256)
@@ -180,11 +183,18 @@ def cpu_baseline(seconds, cores, sims, filter_factor, num_blocks, threads=1, ope
     if os.path.exists(cal):
         with open(cal) as f:
             c = json.load(f)
-        r = c["ratio_reference_over_port"]
-        out["calibration"] = dict(ratio_reference_over_port=r, cores=c["cores"], source=os.path.relpath(cal, HERE),
-                                  reference_equivalent=rate * r,
-                                  note="the reference's own multiprocess pipeline vs this port, timed back to back on "
-                                       "the build container's cores; reference_equivalent = value x ratio")
+        # the reference's own pipeline over the port run the same way (random openings <-> bench mode)
+        port = c["port_bench_mode"] if openings and "port_bench_mode" in c else c["port"]
+        r = c["reference"]["value"] / port["value"]
+        same = cores == c["cores"] and threads == c["reference"]["thread_count"]
+        out["calibration"] = dict(ratio_reference_over_port=r, source=os.path.relpath(cal, HERE),
+                                  calibrated_on=dict(cores=c["cores"], host=c.get("host"), port_sample=port["sample"]),
+                                  reference_equivalent=rate * r if same else None,
+                                  note=("the reference's own multiprocess pipeline vs this port, timed back to back on "
+                                        f"the build container's {c['cores']} cores; "
+                                        + ("reference_equivalent = value x ratio" if same else
+                                           f"not applied here ({cores} cores / {threads} sims in flight differ from "
+                                           "the calibration run; the ratio is from another host)")))
     return out
 
 
@@ -220,6 +230,21 @@ def main():
                          "SURVEY §6); 1 = sequential search (bit-exact to the reference's sequential fixtures)")
     args = ap.parse_args()
     arena_mode = args.mode == "arena"
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU, started here (the driver's `python bench.py --gpus N` form); the ranks
+        # get torchrun's environment and this process never touches the GPU
+        from self_play_reinforcement_learning_amd import distributed as D
+
+        try:
+            D.check_devices(args.gpus)
+        except RuntimeError as e:
+            print(f"bench.py: {e}", file=sys.stderr, flush=True)
+            sys.exit(2)
+        sys.exit(D.launch_script([os.path.abspath(__file__)] + sys.argv[1:], args.gpus))
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}; the launched ranks count",
+              file=sys.stderr, flush=True)
 
     # The CPU baseline runs FIRST, in child processes started before this process touches the GPU
     # (children of a GPU-initialised process must not exec); rank 0 of a 1-process run only.

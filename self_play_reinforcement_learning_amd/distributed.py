@@ -141,28 +141,6 @@ def unpack_moves(rows, cells, n_actions):
     return out
 
 
-def gather_moves(moves, cells, n_actions, dst=0):
-    """Gather every rank's Move records to rank `dst` (others get None)."""
-    if not is_distributed():
-        return moves
-    dev = _comm_device()
-    rows = pack_moves(moves).to(dev)
-    n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=dev)
-    counts = [torch.zeros_like(n) for _ in range(dist.get_world_size())]
-    dist.all_gather(counts, n)
-    counts = [int(c.item()) for c in counts]
-    width = rows.shape[1]
-    mx = max(max(counts), 1)
-    pad = torch.zeros((mx, width), dtype=torch.uint8, device=dev)
-    pad[: rows.shape[0]] = rows
-    bufs = [torch.zeros_like(pad) for _ in counts]
-    dist.all_gather(bufs, pad)
-    if dist.get_rank() != dst:
-        return None
-    allrows = torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0).cpu()
-    return unpack_moves(allrows, cells, n_actions)
-
-
 def row_bytes(cells, n_actions):
     return cells + 4 * n_actions + 8 + 1 + 4 + 8
 
@@ -176,7 +154,8 @@ class MoveExchange:
     (or when `force`): one all_gather of an int64 header [rows, not-done, stats...] per rank, then
     one gather of the rows padded to the largest count, to `dst` only.  On `dst` the rows are
     unpacked on the device and passed to `sink`.  It returns None on plies without a round, else
-    (all ranks done, stats summed over ranks), so loops that end on it stay in step.
+    (all ranks done, stats summed over ranks), so loops that end on it stay in step; in a single
+    process every ply returns (done, stats) (end_ply).
     """
 
     def __init__(self, cells, n_actions, sink=None, every=8, dst=0):
@@ -199,10 +178,16 @@ class MoveExchange:
             self._staged.append(pack_moves(moves))
 
     def end_ply(self, stats_fn=None, done=False, force=False):
+        """Round plies (every `every`-th ply, or `force`) return (all ranks done, statistics summed over
+        ranks); other plies return None under a process group.  In a single process there is nothing
+        to exchange: every ply returns (done, stats), where stats is this process's statistics on
+        round plies and None on the others (stats_fn reads device counters, so it is not called on
+        every ply)."""
         self._plies += 1
-        if not is_distributed():  # nothing to exchange; the local statistics are the engine's counters
-            return bool(done), None
-        if not force and self._plies % self.every:
+        round_ply = force or self._plies % self.every == 0
+        if not is_distributed():
+            return bool(done), ([int(x) for x in stats_fn()] if stats_fn is not None and round_ply else None)
+        if not round_ply:
             return None
         return self.exchange(stats_fn() if stats_fn is not None else [], done)
 
@@ -241,11 +226,113 @@ class MoveExchange:
 
 
 def broadcast_state_dict(module, src=0):
-    """Epoch-boundary weight refresh from the trainer rank (in place)."""
+    """Epoch-boundary weight refresh from the trainer rank (in place): the whole state_dict in ONE
+    flat buffer per dtype (float parameters / buffers; the int64 BatchNorm counters), i.e. one or
+    two broadcasts per epoch instead of one per tensor."""
     if not is_distributed():
         return
+    from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
+
     dev = _comm_device()
-    for t in list(module.state_dict().values()):
-        buf = t.detach().to(dev)
-        dist.broadcast(buf, src=src)
-        t.copy_(buf.to(t.device))
+    groups = {}
+    for t in module.state_dict().values():
+        groups.setdefault(t.dtype, []).append(t)
+    for dt in sorted(groups, key=str):  # the same order on every rank
+        ts = groups[dt]
+        flat = _flatten_dense_tensors([t.detach().reshape(-1) for t in ts]).to(dev)
+        dist.broadcast(flat, src=src)
+        with torch.no_grad():
+            for t, v in zip(ts, _unflatten_dense_tensors(flat, [t.reshape(-1) for t in ts])):
+                t.copy_(v.reshape(t.shape).to(t.device))
+
+
+# ---------------------------------------------------------------- self-launch (one process per GPU)
+def free_port():
+    """A free TCP port on 127.0.0.1 for a local rendezvous."""
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_env(rank, world, port, base=None):
+    """torchrun's per-rank environment for a single-node job (MASTER_ADDR 127.0.0.1)."""
+    env = dict(os.environ if base is None else base)
+    env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+               GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    return env
+
+
+def in_launched_job():
+    """True when this process is already one rank of a launched job (torchrun or a self-launch)."""
+    return "WORLD_SIZE" in os.environ and "RANK" in os.environ
+
+
+def check_devices(n):
+    """One process per GPU: refuse `n` ranks on fewer visible GPUs unless SPMCTS_ALLOW_OVERSUBSCRIBE=1
+    (rehearsals of N ranks on a smaller box; RCCL refuses two ranks on one GPU, so such a rehearsal
+    uses SPMCTS_DIST_BACKEND=gloo).  Counting devices does not initialise the GPU."""
+    have = torch.cuda.device_count()
+    if have < n and os.environ.get("SPMCTS_ALLOW_OVERSUBSCRIBE", "0") != "1":
+        raise RuntimeError(f"{n} ranks requested (one per GPU) but only {have} GPU(s) are visible; set "
+                           f"SPMCTS_ALLOW_OVERSUBSCRIBE=1 (with SPMCTS_DIST_BACKEND=gloo) to rehearse on fewer GPUs")
+    return have
+
+
+def launch_script(argv, n, poll=0.2):
+    """Run `python argv` as n ranks of a single-node job (bench.py --gpus N without torchrun): each
+    child gets RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* as torchrun would set them.  Must be called
+    before this process touches the GPU (the children are started, never exec'd into).  If a rank
+    fails, the others are stopped.  Returns the first non-zero exit code, else 0."""
+    import subprocess
+    import sys
+
+    port = free_port()
+    procs = [subprocess.Popen([sys.executable] + list(argv), env=rank_env(r, n, port)) for r in range(n)]
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code and not rc:
+                    rc = code
+                    for q in procs:  # a lost rank would leave the others waiting in a collective
+                        q.terminate()
+            time.sleep(poll)
+    finally:
+        for p in procs:
+            p.kill()
+    return rc
+
+
+def _spawned_rank(rank, world, port, fn, args, kwargs):
+    os.environ.update(rank_env(rank, world, port, base={}))
+    fn(*args, **kwargs)
+
+
+def spawn_ranks(fn, n, *args, **kwargs):
+    """Run fn(*args, **kwargs) in n fresh processes (spawn), rank r with torchrun's environment: how
+    SelfPlayScheduler starts one process per GPU itself, as the reference's scheduler starts its
+    own worker processes (self_play_parallel.py:95-171).  fn and its arguments must pickle; CPU
+    tensors travel by shared memory.  Raises if any rank fails."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    port = free_port()
+    procs = [ctx.Process(target=_spawned_rank, args=(r, n, port, fn, args, kwargs)) for r in range(n)]
+    for p in procs:
+        p.start()
+    failed = []
+    for r, p in enumerate(procs):
+        p.join()
+        if p.exitcode:
+            failed.append((r, p.exitcode))
+            for q in procs:
+                if q.is_alive():
+                    q.terminate()
+    if failed:
+        raise RuntimeError(f"rank process(es) failed: {failed}")

@@ -130,6 +130,11 @@ class SelfPlayEngine:
         # simulation step; by default on when every evaluator is a pure, batch-independent function of
         # the leaf planes (the fused HIP trunk), so each leaf still gets exactly its own outputs
         pure = all(getattr(ev, "pure_planes", False) for ev in (self.evaluator, self.evaluator1) if ev is not None)
+        if leaf_dedup and not pure:
+            # an evaluator whose outputs depend on the batch or the row (the torch TowerEvaluator's
+            # batch-shaped heads, the per-row salted table net) would hand a duplicate its owner's outputs
+            raise ValueError("leaf_dedup=True needs evaluators that are pure functions of the leaf planes "
+                             "(pure_planes); leave it None to enable it only where that holds")
         self.leaf_dedup = bool(pure if leaf_dedup is None else leaf_dedup) and self.search_threads > 1
         if self.leaf_dedup:
             self.arena.set_leaf_dedup(True)

@@ -4,7 +4,7 @@ The reference moves every `Move` record through a multiprocessing queue into a
 Python `deque` (rl_utils/memory.py:8-33) and samples `batch_size` of them per
 update with `np.random.choice(len, k, replace=False)` (:26-30), stacking the
 tensors again for the loss (mcts.py:234-252).  Here the arena's exported Move
-rows (`Arena.export_moves` / `distributed.gather_moves`: state int8 [n, cells],
+rows (`Arena.export_moves` / `distributed.MoveExchange`: state int8 [n, cells],
 tree_probs f32 [n, A], q f64 + dtype flag, z f32) are appended to fixed device
 tensors, and a training batch is one uniform sample without replacement
 (`torch.randperm`) gathered on the device.

@@ -21,9 +21,18 @@ signatures.  What changes is underneath:
     plies on the same GPU; self-play uses the epoch-start weights, refreshed at
     each epoch boundary exactly like the reference's epoch_value reload.
 
-With torchrun and WORLD_SIZE > 1, every rank plays its own shard of games;
-Move records and episode statistics are gathered to rank 0 (distributed.py).
+Multi-GPU: one process per GPU.  Under torchrun (WORLD_SIZE > 1) every rank plays
+its own shard of games; Move records and episode statistics are gathered to
+rank 0 (distributed.py).  Without torchrun, `train_model` / `compare_models`
+start the rank processes themselves (`gpus=`; default: every visible GPU), as
+the reference's scheduler starts its own worker processes
+(self_play_parallel.py:95-171, num_workers = cpu_count()): the children rebuild
+this scheduler from its constructor arguments (networks copied to the host),
+rank 0 checkpoints, and the parent's network is updated from the last
+checkpoint afterwards, as the reference's shared-memory network is updated by
+its UpdateWorker process.
 """
+import copy
 import datetime
 import logging
 import os
@@ -82,7 +91,10 @@ class SelfPlayScheduler:
     def __init__(self, policy_container, env, evaluation_policy_container=None, network=None, swap_sides=True,
                  save_dir="saves", epoch_length=500, initial_games=64, lr=0.001, stagger=False, evaluation_games=100,
                  evaluation_network=None, stagger_mem_step=5000, deduplicate=False, update_delay=0.01,
-                 self_play=None, n_games=None, device=None, seed=0, updates_per_ply=4, lanes=None, exchange_every=8):
+                 self_play=None, n_games=None, device=None, seed=0, updates_per_ply=4, lanes=None, exchange_every=8,
+                 gpus=None, start_time=None):
+        # constructor arguments, for rank processes started by this scheduler (_run_ranks)
+        self._init_kwargs = {k: v for k, v in locals().items() if k not in ("self", "__class__")}
         self.policy_container = policy_container
         self.evaluation_policy_container = evaluation_policy_container
         self.env_gen = env
@@ -106,11 +118,14 @@ class SelfPlayScheduler:
         # >1: LanedEngine (arenas on separate HIP streams, each a complete arena); None = 2 lanes for
         # arenas of >= 1,024 games, where the overlap pays (bench.py), else one arena
         self.lanes = None if lanes is None else max(1, int(lanes))
+        if D.in_launched_job() and int(D.env_rank()[1]) > 1:
+            D.init_from_env()  # one rank of a torchrun / self-launched job
         rank, world, local = D.env_rank()
         self.rank, self.world = rank, world
+        self.gpus = gpus
         self.device = torch.device(device) if device is not None else D.local_device()
         self.n_games = n_games
-        self.start_time = datetime.datetime.now().isoformat()
+        self.start_time = start_time or datetime.datetime.now().isoformat()
         self.task_queue = LocalQueue()
         self.memory_queue = LocalQueue()
         self.result_queue = LocalQueue()
@@ -192,7 +207,13 @@ class SelfPlayScheduler:
                       and (not prev_run or os.path.basename(d) != self.start_time) and os.listdir(d))
         if not runs:
             return None
-        saves = sorted(glob(os.path.join(runs[-1], "model*")))
+        return self._load_checkpoint(runs[-1])
+
+    def _load_checkpoint(self, run_dir):
+        """The newest `model-<iso>:<games>` of one run folder (base_worker.py:44-62) into the network."""
+        from glob import glob
+
+        saves = sorted(glob(os.path.join(run_dir, "model*")))
         if not saves:
             return None
         ck = torch.load(saves[-1], weights_only=True, map_location="cpu")
@@ -228,9 +249,58 @@ class SelfPlayScheduler:
         eng.play_games(per_rank, on_moves=on_moves, on_ply=on_ply, every=self.exchange_every)
         eng.check()
 
+    # ------------------------------------------------------------------ one process per GPU
+    def _ranks(self, gpus):
+        """How many rank processes this call starts: 1 (run here) inside a launched job; else `gpus`
+        (the call's, then the constructor's; None = every visible GPU)."""
+        if D.in_launched_job() or D.is_distributed():
+            return 1
+        n = gpus if gpus is not None else self.gpus
+        if n is None:
+            n = torch.cuda.device_count()  # counting devices does not initialise the GPU
+        return max(1, int(n))
+
+    def _spawn_kwargs(self):
+        """Constructor arguments for the rank processes: modules copied to the host (CPU tensors travel
+        to spawned processes by shared memory), the same start_time (one checkpoint folder)."""
+        def host(obj):
+            if isinstance(obj, torch.nn.Module):
+                return copy.deepcopy(obj).cpu()
+            if isinstance(obj, dict):
+                return {k: host(v) for k, v in obj.items()}
+            if isinstance(obj, (list, tuple)):
+                return type(obj)(host(v) for v in obj)
+            if hasattr(obj, "policy_kwargs"):  # ModelContainer
+                c = copy.copy(obj)
+                c.policy_kwargs = host(obj.policy_kwargs)
+                return c
+            return obj
+
+        kw = {k: host(v) for k, v in self._init_kwargs.items()}
+        kw.update(network=host(self.network), start_time=self.start_time, device=None, gpus=1)
+        return kw
+
+    def _run_ranks(self, n, method, kwargs):
+        D.check_devices(n)
+        import multiprocessing as mp
+
+        q = mp.get_context("spawn").Queue()
+        D.spawn_ranks(_scheduler_rank, n, self._spawn_kwargs(), method, kwargs, q)
+        return q.get(timeout=60)
+
     def train_model(self, num_epochs=10, resume_model=False, resume_memory=False, num_workers=None,
-                    threads_per_worker=8, inference_proxy=True):
-        """self_play_parallel.py:213-291"""
+                    threads_per_worker=8, inference_proxy=True, gpus=None):
+        """self_play_parallel.py:213-291.  gpus > 1 (default: every visible GPU) outside a launched
+        job: one rank process per GPU (_run_ranks); this scheduler's network then holds the final
+        checkpoint's weights."""
+        n = self._ranks(gpus)
+        if n > 1:
+            self._run_ranks(n, "train_model", dict(num_epochs=num_epochs, resume_model=resume_model,
+                                                    resume_memory=resume_memory, num_workers=num_workers,
+                                                    threads_per_worker=threads_per_worker,
+                                                    inference_proxy=inference_proxy))
+            self._load_checkpoint(os.path.join(self.save_dir, self.start_time))
+            return None
         self.setup_player_workers(num_workers=num_workers, threads_per_worker=threads_per_worker,
                                   resume_model=resume_model, inference_proxy=inference_proxy)
         self.setup_update_worker(resume_memory=resume_memory, resume_model=resume_model)
@@ -253,6 +323,10 @@ class SelfPlayScheduler:
                 m = self.trainer.memory
                 m.change_size(min(m.max_size + self.stagger_mem_step, 1500000))
             if self.deduplicate:
+                if epoch == 0:
+                    logging.warning("deduplicate=True merges duplicate boards of the replay ring; the reference's "
+                                    "own deduplicate() raises TypeError with its Move type (memory.py:93) and merges "
+                                    "nothing, so training data differs from the reference's from here on")
                 # updateworker.py:88-89 calls policy.deduplicate() here; with the reference's own Move
                 # that raises TypeError (memory.py:93: the rebuilt tuple lacks q) and, caught, skips the
                 # checkpoint.  The device ring merges duplicate boards (z, tree_probs and q averaged);
@@ -360,15 +434,34 @@ class SelfPlayScheduler:
         total, _ = self.parse_results(reward_list)
         return total
 
-    def compare_models(self, num_workers=None, inference_proxy=True, threads_per_worker=8, resume_model=False):
+    def compare_models(self, num_workers=None, inference_proxy=True, threads_per_worker=8, resume_model=False,
+                       gpus=None):
         """self_play_parallel.py:355-379: epoch_length evaluation games, policy network vs the
         evaluation policy (a second network on the same arena, or a hard-coded player).
-        Returns (total_rewards, breakdown) exactly as the reference's parse_results."""
+        Returns (total_rewards, breakdown) exactly as the reference's parse_results; with gpus > 1
+        the games are sharded over one rank process per GPU."""
+        n = self._ranks(gpus)
+        if n > 1:
+            return self._run_ranks(n, "compare_models", dict(num_workers=num_workers, inference_proxy=inference_proxy,
+                                                              threads_per_worker=threads_per_worker,
+                                                              resume_model=resume_model))
         if resume_model:
             self._load_latest(prev_run=True)
         self._resolve_threads(inference_proxy)  # evaluation workers talk to the InferenceProxy too
         reward_list = self._play_evaluation(self.epoch_length)
         return self.parse_results(reward_list)
+
+
+def _scheduler_rank(kwargs, method, call_kwargs, result_q):
+    """One rank process of SelfPlayScheduler._run_ranks (the environment holds RANK / WORLD_SIZE)."""
+    sp = SelfPlayScheduler(**kwargs)
+    try:
+        out = getattr(sp, method)(**call_kwargs)
+        if sp.rank == 0:
+            result_q.put(out)
+    finally:
+        if D.is_distributed():
+            torch.distributed.destroy_process_group()
 
 
 class _Trainer:

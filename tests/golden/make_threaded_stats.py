@@ -40,6 +40,13 @@ one game thread this is rare; with 8 game threads contending for the GIL it is f
 and it measurably flattens the root visit distribution.
 
 Only inputs and the outputs the reference produced are written (no reference source).
+
+Round 3: resnet_single holds 1,000 searches per position (was 160), made with one process per
+position side by side (OMP_NUM_THREADS=2 each) and merged:
+
+    for p in 0 1 2; do OMP_NUM_THREADS=2 python tests/golden/make_threaded_stats.py \
+        resnet_single 1000 $p /tmp/g6_rs_$p.json & done; wait
+    python tests/golden/make_threaded_stats.py merge resnet_single /tmp/g6_rs_{0,1,2}.json
 """
 import concurrent.futures
 import json
@@ -137,7 +144,7 @@ class _ReexpansionCounter:
         return dict(expansions=self.calls, re_expansions=self.re)
 
 
-def run_threaded(net_module, samples, label, game_threads):
+def run_threaded(net_module, samples, label, game_threads, positions=POSITIONS):
     """The reference's serving structure: InferenceWorker process + proxy + game threads."""
     from games.algos.inference_proxy import InferenceProxy
     from games.algos.inference_worker import InferenceWorker
@@ -154,7 +161,7 @@ def run_threaded(net_module, samples, label, game_threads):
     lock = threading.Lock()
     t0 = time.time()
     try:
-        for opening in POSITIONS:
+        for opening in positions:
             counter = _ReexpansionCounter()
             res = []
 
@@ -213,11 +220,34 @@ def _rounded(data):
     return data
 
 
+def run_part(name, samples, pi, out):
+    """One position of a resnet set in its own process (several run side by side on the host's cores;
+    `merge` joins the parts): `resnet_single <samples> <position> <out.json>`."""
+    gt = {"resnet_single": 1, "resnet_serving": GAME_THREADS}[name]
+    net, sums = _resnet()
+    pos = run_threaded(net, samples, f"{name}[{pi}]", gt, positions=[POSITIONS[pi]])
+    json.dump(dict(threads_per_worker=gt, net_checksums=sums, position=pos[0]), open(out, "w"))
+
+
+def merge(name, parts):
+    """Replace set `name` in the fixture by the positions of the part files (in position order)."""
+    data = json.load(open(OUT))
+    ps = [json.load(open(f)) for f in parts]
+    data[name] = dict(sims=SIMS, thread_count=THREADS, game="connect4", threads_per_worker=ps[0]["threads_per_worker"],
+                      net="ResidualTower(7,6,7,num_blocks=20,filter_factor=32) seed 0",
+                      net_checksums=ps[0]["net_checksums"], positions=[p["position"] for p in ps])
+    json.dump(_rounded(data), open(OUT, "w"), separators=(",", ":"))
+
+
 def main():
     torch.multiprocessing.set_start_method("spawn")  # as the reference's entry points (main.py:109)
     os.chdir("/tmp")  # reference modules may write logs into cwd
     os.makedirs("/tmp/g6_saves", exist_ok=True)
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if which == "merge":  # merge <set> <part0.json> <part1.json> ...
+        return merge(sys.argv[2], sys.argv[3:])
+    if len(sys.argv) == 5:  # <set> <samples> <position> <out.json>
+        return run_part(which, int(sys.argv[2]), int(sys.argv[3]), sys.argv[4])
     data = json.load(open(OUT)) if os.path.exists(OUT) else {}
     common = dict(sims=SIMS, thread_count=THREADS, game="connect4")
     np.random.seed(6)

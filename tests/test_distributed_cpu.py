@@ -1,7 +1,8 @@
 """CPU: the multi-GPU exchange steps with torch.distributed gloo, world sizes 2 and 4: the
 episode-batch MoveExchange (Move rows staged per rank, one header all_gather + one gather to rank 0
 per round, statistics summed in the same round), the engines' play_games loops that end on it,
-and the primitives (stats all_reduce, Move gather, max, weight broadcast)."""
+the primitives (stats all_reduce, max, one-buffer weight broadcast), and the self-launch helpers that
+start one process per GPU (bench.py --gpus N, SelfPlayScheduler(gpus=N))."""
 import os
 import tempfile
 
@@ -57,14 +58,16 @@ def _worker(rank, world, port, q):
                       SPMCTS_DIST_INIT="file://" + port)
     D.init_from_env(backend="gloo")
     stats = D.all_reduce_stats([rank + 1, 10 * rank, 1, 0, 0, 0, 1, 0])
-    got = D.gather_moves(_moves(rank, 3 + 2 * rank), 42, 7)
     mx = D.all_reduce_max(float(rank) * 1.5)
-    net = torch.nn.Linear(4, 2)
+    net = torch.nn.Sequential(torch.nn.Linear(4, 2), torch.nn.BatchNorm1d(2))  # float + int64 state
     with torch.no_grad():
-        net.weight.fill_(float(rank))
+        net[0].weight.fill_(float(rank))
+        net[1].running_mean.fill_(float(rank) + 0.5)
+        net[1].num_batches_tracked.fill_(7 + rank)
     D.broadcast_state_dict(net)
-    q.put(_by_value((rank, stats.tolist(), None if got is None else {k: v.clone() for k, v in got.items()}, mx,
-                     float(net.weight.sum()))))
+    sd = net.state_dict()
+    q.put(_by_value((rank, stats.tolist(), None, mx, float(net[0].weight.sum()),
+                     [float(sd["1.running_mean"].sum()), int(sd["1.num_batches_tracked"])])))
     torch.distributed.destroy_process_group()
 
 
@@ -250,11 +253,89 @@ def test_exchange_primitives_gloo(world):
     assert all(r[1] == want for r in res)
     assert all(r[3] == 1.5 * (world - 1) for r in res)
     assert all(r[4] == 0.0 for r in res)  # rank 0's weights everywhere
-    assert all(r[2] is None for r in res[1:])
-    g0 = res[0][2]
-    exp = {k: torch.cat([_moves(r, 3 + 2 * r)[k] for r in range(world)]) for k in g0}
-    for k in exp:
-        assert torch.equal(g0[k].reshape(exp[k].shape), exp[k]), k
+    assert all(r[5] == [1.0, 7] for r in res)  # float buffers and the int64 counter too
+
+
+def test_end_ply_single_process():
+    """Without a process group every ply returns (done, stats): this process's statistics on round
+    plies (every `every`-th, or forced), None on the others; the sink gets the rows at once."""
+    got = []
+    ex = D.MoveExchange(42, 7, sink=lambda m: got.append(int(m["z"].shape[0])), every=3)
+    calls = []
+
+    def stats():
+        calls.append(1)
+        return [5, 6]
+
+    out = []
+    for ply in range(4):
+        ex.stage(_moves(ply, ply))
+        out.append(ex.end_ply(stats, done=ply == 3))
+    out.append(ex.end_ply(stats, done=True, force=True))
+    assert out == [(False, None), (False, None), (False, [5, 6]), (True, None), (True, [5, 6])]
+    assert len(calls) == 2
+    assert got == [1, 2, 3] and ex.rows_gathered == 6
+
+
+def test_rank_env_and_device_check(monkeypatch):
+    env = D.rank_env(3, 8, 12345, base={"X": "1"})
+    assert env == {"X": "1", "RANK": "3", "LOCAL_RANK": "3", "WORLD_SIZE": "8", "LOCAL_WORLD_SIZE": "8",
+                   "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "12345"}
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    monkeypatch.delenv("SPMCTS_ALLOW_OVERSUBSCRIBE", raising=False)
+    with pytest.raises(RuntimeError, match="only 1 GPU"):
+        D.check_devices(8)
+    monkeypatch.setenv("SPMCTS_ALLOW_OVERSUBSCRIBE", "1")
+    assert D.check_devices(8) == 1
+
+
+_CHILD = """
+import os, sys, torch.distributed as dist
+sys.path.insert(0, {repo!r})
+from self_play_reinforcement_learning_amd import distributed as D
+rank, world, local = D.init_from_env(backend="gloo")
+s = D.all_reduce_stats([1, rank])
+open(os.path.join({out!r}, "rank%d" % rank), "w").write(" ".join(
+    [os.environ["RANK"], os.environ["LOCAL_RANK"], os.environ["WORLD_SIZE"], os.environ["MASTER_ADDR"],
+     str(world), str(D.is_distributed())] + [str(int(x)) for x in s]))
+dist.destroy_process_group()
+sys.exit(int(os.environ.get("FAIL_RANK", "-1")) == rank and 3 or 0)
+"""
+
+
+def test_launch_script_wires_ranks(tmp_path):
+    """bench.py's self-launch: N child processes of one script with torchrun's environment, one
+    rendezvous on 127.0.0.1, a collective across them; a failing rank's exit code comes back."""
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "child.py"
+    script.write_text(_CHILD.format(repo=repo, out=str(tmp_path)))
+    assert D.launch_script([str(script)], 3) == 0
+    for r in range(3):
+        f = (tmp_path / f"rank{r}").read_text().split()
+        assert f == [str(r), str(r), "3", "127.0.0.1", "3", "True", "3", "3"]
+    os.environ["FAIL_RANK"] = "1"
+    try:
+        assert D.launch_script([str(script)], 2) == 3
+    finally:
+        del os.environ["FAIL_RANK"]
+
+
+def _spawn_target(out, tag):
+    rank, world, _ = D.init_from_env(backend="gloo")
+    s = D.all_reduce_stats([rank])
+    with open(os.path.join(out, f"{tag}{rank}"), "w") as f:
+        f.write(f"{rank} {world} {int(s[0])}")
+    torch.distributed.destroy_process_group()
+    if tag == "fail" and rank == 1:
+        raise SystemExit(5)
+
+
+def test_spawn_ranks(tmp_path):
+    """SelfPlayScheduler's self-spawn: fn runs in N spawned processes as ranks 0..N-1."""
+    D.spawn_ranks(_spawn_target, 2, str(tmp_path), "ok")
+    assert sorted((tmp_path / f"ok{r}").read_text() for r in range(2)) == ["0 2 1", "1 2 1"]
+    with pytest.raises(RuntimeError, match="failed"):
+        D.spawn_ranks(_spawn_target, 2, str(tmp_path), "fail")
 
 
 def _exchange_worker(rank, world, port, q):
@@ -309,3 +390,35 @@ def test_move_exchange_rounds_gloo(world):
     for g, e in zip(got, nonempty):
         for k in e:
             assert torch.equal(g[k].reshape(e[k].shape), e[k]), k
+
+
+def test_scheduler_rank_count_and_spawn_kwargs(tmp_path, monkeypatch):
+    """SelfPlayScheduler(gpus=...): how many rank processes train_model / compare_models start (1 inside
+    a launched job; else the call's gpus, the constructor's, or every visible GPU), and the constructor
+    arguments the ranks rebuild it from (networks as host copies, one start_time, gpus=1) pickle."""
+    import pickle
+
+    from self_play_reinforcement_learning_amd import ModelContainer, ResidualTower
+    from self_play_reinforcement_learning_amd.envs import Connect4Env
+    from self_play_reinforcement_learning_amd.mcts import MCTreeSearch
+    from self_play_reinforcement_learning_amd.self_play_parallel import SelfPlayScheduler
+
+    for k in ("WORLD_SIZE", "RANK"):
+        monkeypatch.delenv(k, raising=False)
+    net = ResidualTower(7, 6, 7, num_blocks=1, filter_factor=4)
+    ev = ModelContainer(MCTreeSearch, policy_kwargs=dict(network=ResidualTower(7, 6, 7, num_blocks=1, filter_factor=4),
+                                                          env=Connect4Env, iterations=10))
+    sp = SelfPlayScheduler(ModelContainer(MCTreeSearch, policy_kwargs=dict(env=Connect4Env, iterations=10)),
+                           Connect4Env, evaluation_policy_container=ev, network=net, save_dir=str(tmp_path), gpus=3)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    assert sp._ranks(None) == 3 and sp._ranks(2) == 2 and sp._ranks(1) == 1
+    sp.gpus = None
+    assert sp._ranks(None) == 8
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    monkeypatch.setenv("RANK", "0")
+    assert sp._ranks(4) == 1  # already one rank of a launched job
+    kw = pickle.loads(pickle.dumps(sp._spawn_kwargs()))
+    assert kw["gpus"] == 1 and kw["start_time"] == sp.start_time and kw["device"] is None
+    assert kw["network"] is not net and torch.equal(kw["network"].conv1.weight, net.conv1.weight)
+    assert kw["evaluation_policy_container"].policy_kwargs["iterations"] == 10
+    assert isinstance(kw["evaluation_policy_container"].policy_kwargs["network"], ResidualTower)

@@ -150,6 +150,38 @@ def test_scheduler_train_model_dropin(tmp_path, lanes):
     assert m[0].state.shape == (7, 6) and m[0].tree_probs.shape == (7,) and m[0].actual_val.dtype == torch.float32
 
 
+def test_scheduler_spawns_rank_processes(tmp_path, monkeypatch):
+    """SelfPlayScheduler(gpus=2) outside torchrun starts its own two rank processes (the reference's
+    scheduler starts its worker processes itself, self_play_parallel.py:95-171); rehearsed on the box's
+    one GPU over gloo (RCCL refuses two ranks per GPU).  Both ranks play their share, rank 0 owns the
+    replay and checkpoints, and the parent's network holds the final checkpoint afterwards; then
+    compare_models shards its games over two ranks and returns the parent's parse_results."""
+    from self_play_reinforcement_learning_amd import (Connect4Env, MCTreeSearch, ModelContainer, OneStepLookahead,
+                                                      ResidualTower, SelfPlayScheduler)
+
+    monkeypatch.setenv("SPMCTS_ALLOW_OVERSUBSCRIBE", "1")
+    monkeypatch.setenv("SPMCTS_DIST_BACKEND", "gloo")
+    torch.manual_seed(0)
+    network = ResidualTower(width=7, height=6, action_size=7, num_blocks=1, filter_factor=4)
+    before = {k: v.clone() for k, v in network.state_dict().items()}
+    container = ModelContainer(policy_gen=MCTreeSearch, policy_kwargs=dict(iterations=8, min_memory=32, memory_size=3000,
+                                                                           env=Connect4Env, batch_size=16))
+    ev = ModelContainer(policy_gen=OneStepLookahead, policy_kwargs=dict(env=Connect4Env))
+    sp = SelfPlayScheduler(env=Connect4Env, network=network, policy_container=container, evaluation_policy_container=ev,
+                           initial_games=8, epoch_length=16, evaluation_games=0, save_dir=str(tmp_path), lr=0.005,
+                           n_games=8, gpus=2)
+    sp.train_model(1)
+    saves = sorted(p for p in (tmp_path / sp.start_time).iterdir() if p.name.startswith("model-"))
+    assert len(saves) == 1
+    ck = torch.load(saves[-1], weights_only=True)
+    for k, v in network.state_dict().items():
+        assert torch.equal(v.cpu(), ck["model"][k].cpu()), k
+    assert any(not torch.equal(before[k], v.cpu()) for k, v in network.state_dict().items())
+    total, breakdown = sp.compare_models(gpus=2)
+    assert sum(v for side in breakdown.values() for v in side.values()) == 16
+    assert sum(breakdown["first"].values()) == 8 and sum(breakdown["second"].values()) == 8
+
+
 def _tower(seed, blocks=2, ff=32):
     torch.manual_seed(seed)
     return ResidualTowerCls()(7, 6, 7, num_blocks=blocks, filter_factor=ff).cuda().eval()
