@@ -224,6 +224,9 @@ def main():
                     help="node blocks per tree; below the worst case the arena recycles subtrees (k_compact)")
     ap.add_argument("--no-pack", action="store_true",
                     help="lanes > 1: keep round-aligned tower tiles (no SPMCTS_TOWER_PACK)")
+    ap.add_argument("--dtype", choices=["bf16", "fp16"], default="bf16",
+                    help="element type of the fused trunk's weights / activations (fp32 accumulation); fp16 is the "
+                         "reference's own inference dtype (amp.autocast, inference_worker.py:117)")
     ap.add_argument("--search-threads", type=int, default=4,
                     help="sims in flight per tree with virtual loss: the reference's thread_count search "
                          "(mcts.py:328-331), 4 in its headline self-play setup (InferenceProxy workers, "
@@ -270,7 +273,8 @@ def main():
     if arena_mode:  # BASELINE config 5: two frozen nets, greedy (evaluate-mode) MCTS on both sides
         torch.manual_seed(1)
         opponent = ResidualTower(7, 6, 7, num_blocks=args.blocks, filter_factor=args.filter_factor).to(dev).eval()
-    kw = dict(iterations=args.sims, seed=1234 + rank, device=dev, bucket=args.bucket, opponent=opponent,
+    tdt = {"bf16": torch.bfloat16, "fp16": torch.float16}[args.dtype]
+    kw = dict(iterations=args.sims, seed=1234 + rank, device=dev, bucket=args.bucket, opponent=opponent, dtype=tdt,
               evaluate=arena_mode, record=not arena_mode, search_threads=args.search_threads,
               blocks_per_tree=args.blocks_per_tree, leaf_dedup=False if args.no_leaf_dedup else None)
     if args.lanes > 1:
@@ -389,11 +393,11 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": args.dtype,
         "data": "synthetic (self-generated games, random-init ResNet weights, torch.manual_seed(0))",
         "config": {
             "workload": f"connect4 7x6 self-play, {args.sims} sims/move, {args.games} concurrent games per GPU "
-                        f"(2 trees each), ResNet-{4 * args.filter_factor}x{args.blocks} bf16 leaf eval, fp64 tree stats",
+                        f"(2 trees each), ResNet-{4 * args.filter_factor}x{args.blocks} {args.dtype} leaf eval, fp64 tree stats",
             "games_per_gpu": args.games,
             "global_games": args.games * world,
             "sims_per_move": args.sims,
@@ -404,7 +408,7 @@ def main():
             "leaf_dedup": bool(getattr(eng, "leaf_dedup", False)),
         },
         "roofline": {
-            "kernel": f"tower::k_tower_dyn (fused ResNet-{4 * args.filter_factor}x{args.blocks} trunk, bf16 MFMA)",
+            "kernel": f"tower::k_tower_dyn (fused ResNet-{4 * args.filter_factor}x{args.blocks} trunk, {args.dtype} MFMA)",
             "bound": "mfma",
             "achieved": tw_tflops,
             "peak": BF16_DENSE_PEAK_TFLOPS,

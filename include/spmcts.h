@@ -249,21 +249,24 @@ int spmcts_table_net(int32_t game, int32_t width, int32_t height, const void *le
 /* Fused residual-tower trunk for leaf evaluation (games/general/modules.py:43-107
  * with BatchNorm folded): stem conv3x3 + num_blocks BasicBlocks + the policy/value
  * 1x1 head convs, bias + ReLU (+ residual) fused, activations resident in LDS,
- * bf16 MFMA with fp32 accumulation.  planes_dev: bf16 [batch][W][H][3] (NHWC
- * leaf rows); features_dev: bf16 [batch][W*H][channels/2] (policy | value head
- * channels, cell-major).  Packed weight/bias layout: csrc/tower.hip.  Instantiated
- * for 7x6 and 3x3 boards with channels 128 or 256. */
+ * bf16 (or, with SPMCTS_TOWER_F16, fp16 = the reference's autocast dtype,
+ * inference_worker.py:117) MFMA with fp32 accumulation.  planes_dev: bf16 [batch][W][H][3]
+ * (NHWC leaf rows, 0/1 planes); weights and features_dev [batch][W*H][channels/2] (policy |
+ * value head channels, cell-major) in the flags' element type.  Packed weight/bias layout:
+ * csrc/tower.hip.  Instantiated for 7x6 and 3x3 boards with channels 128 or 256. */
+#define SPMCTS_TOWER_F16 2
 int spmcts_tower_forward(int32_t width, int32_t height, int32_t channels, int32_t n_blocks, const void *planes_dev,
                          int32_t batch, const void *weights_dev, const float *bias_dev, void *features_dev,
-                         spmcts_stream stream);
+                         int32_t flags, spmcts_stream stream);
 /* The linear heads on the trunk features (modules.py:96-105), fused: policy softmax over
  * `actions` and tanh value.  head_w: bf16 rows [32 (policy, zero-padded)] ++ [8ff] over K = W*H*ff
  * columns in (cell, channel) order, fragment-swizzled: for 32-row tile j and 16-column step s, one
  * contiguous 1 KiB block whose 16-byte lane l holds row 32j + (l % 32), columns 16s + 8(l / 32) .. +8;
- * head_b: f32 bp[32] ++ bv[8ff] ++ wo[8ff] ++ bo. */
+ * head_b: f32 bp[32] ++ bv[8ff] ++ wo[8ff] ++ bo.  flags: SPMCTS_TOWER_F16 = features and head_w
+ * are fp16 (else bf16). */
 int spmcts_tower_heads(int32_t width, int32_t height, int32_t channels, int32_t actions, const void *features_dev,
                        int32_t batch, const void *head_w_dev, const float *head_b_dev, float *probs_dev,
-                       float *values_dev, spmcts_stream stream);
+                       float *values_dev, int32_t flags, spmcts_stream stream);
 /* Head epilogue after one GEMM Z = features @ Wc^T (Wc rows: value hidden [hidden] then
  * policy [actions]): value = tanh(relu(Z[:hidden] + bv) . wo + bo), probs = softmax(Z[hidden:] + bp).
  * z_dev bf16 [batch][ldz]; head_b: f32 bv[hidden] ++ wo[hidden] ++ bo ++ bp[actions]. */
@@ -274,14 +277,16 @@ int spmcts_tower_supported(int32_t width, int32_t height, int32_t channels);
  * spmcts_select) so no host synchronisation is needed; max_batch bounds the grid.
  * flags: SPMCTS_TOWER_PACK = the launch shares the chip with concurrent launches on other streams
  * (engine.LanedEngine): every board goes in full-size tiles and only the last few boards in one
- * smaller tile, instead of whole chip rounds of full tiles plus one round of smaller tiles. */
+ * smaller tile, instead of whole chip rounds of full tiles plus one round of smaller tiles;
+ * SPMCTS_TOWER_F16 = fp16 weights / activations / features. */
 #define SPMCTS_TOWER_PACK 1
 int spmcts_tower_forward_dev(int32_t width, int32_t height, int32_t channels, int32_t n_blocks, const void *planes_dev,
                              const int32_t *count_dev, int32_t max_batch, const void *weights_dev,
                              const float *bias_dev, void *features_dev, int32_t flags, spmcts_stream stream);
 int spmcts_tower_heads_dev(int32_t width, int32_t height, int32_t channels, int32_t actions, const void *features_dev,
                            const int32_t *count_dev, int32_t max_batch, const void *head_w_dev,
-                           const float *head_b_dev, float *probs_dev, float *values_dev, spmcts_stream stream);
+                           const float *head_b_dev, float *probs_dev, float *values_dev, int32_t flags,
+                           spmcts_stream stream);
 /* Memory-roofline helper: device copy bandwidth probe (bytes each way). */
 int spmcts_copy_probe(const void *src_dev, void *dst_dev, uint64_t bytes, spmcts_stream stream);
 

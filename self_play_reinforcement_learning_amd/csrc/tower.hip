@@ -52,11 +52,56 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef short i16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+// Element type of the weights, the LDS activations and the head features: bf16, or fp16 = the
+// reference's own inference dtype (amp.autocast, inference_worker.py:117).  Operands travel in 16-byte
+// containers typed bf16x8 whatever E is (a bit cast at the MFMA is free); both MFMA forms take the
+// same cycles on gfx950 (MI355X_MICROARCH.md).  fp32 accumulation either way.
+template <class E>
+struct Ty;
+template <>
+struct Ty<__bf16> {
+  static constexpr bool BF16 = true;
+  static __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+  // relu of a pair, packed (v_cvt_pk_bf16_f32 + v_pk_max_i16: a negative bf16 is a negative int16)
+  static __device__ __forceinline__ uint32_t relu_pk(f32x2 v) {
+    const bf16x2 b = __builtin_convertvector(v, bf16x2);
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(i16x2, b), i16x2{0, 0}));
+  }
+  static __device__ __forceinline__ f32x2 unpk(uint32_t x) {
+    return f32x2{__uint_as_float(x << 16), __uint_as_float(x & 0xffff0000u)};
+  }
+  static __device__ __forceinline__ uint16_t from_bf16(__bf16 x) { return __builtin_bit_cast(uint16_t, x); }
+};
+template <>
+struct Ty<_Float16> {
+  static constexpr bool BF16 = false;
+  static __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                  0);
+  }
+  // round to nearest even (as torch's fp16 casts), then relu as a signed 16-bit max with 0
+  static __device__ __forceinline__ uint32_t relu_pk(f32x2 v) {
+    const f16x2 b = __builtin_convertvector(v, f16x2);
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(i16x2, b), i16x2{0, 0}));
+  }
+  static __device__ __forceinline__ f32x2 unpk(uint32_t x) {
+    return __builtin_convertvector(__builtin_bit_cast(f16x2, x), f32x2);
+  }
+  static __device__ __forceinline__ uint16_t from_bf16(__bf16 x) {
+    return __builtin_bit_cast(uint16_t, (_Float16)(float)x);
+  }
+};
 
 
 template <int C_, int ROWS_, int W_, int H_, int CG_ = 2, int WAVES_ = 4, int ABL_ = 0, int DEPTH_ = 4, int OCC_ = 1,
-          bool XMAJ_ = false, bool EDGE_ = false>
-struct Cfg {
+          bool XMAJ_ = false, bool EDGE_ = false, class E_ = __bf16>
+struct Cfg : Ty<E_> {
+  using E = E_;  // operand / activation element type (Ty)
   static constexpr int OCC = OCC_;  // resident workgroups per CU the register budget is sized for
   static constexpr int DEPTH = DEPTH_;  // weight-fragment prefetch distance (k-steps)
   static constexpr int C = C_, ROWS = ROWS_, W = W_, H = H_;
@@ -223,12 +268,13 @@ __device__ __forceinline__ void acc_init(f32x16 (&acc)[K::MT][K::NT], const char
       for (int t = 0; t < K::NT; ++t) {
         float v0 = bv.x, v1 = bv.y, v2 = bv.z, v3 = bv.w;
         if (RESID) {
-          const bf16x4 x = *(const bf16x4 *)(dst + (((wave / K::CG) * K::NT + t) * 32 + r) * K::RS +
-                                             phys_off((wave % K::CG) * K::MT + m, h, g));
-          v0 += (float)x[0];
-          v1 += (float)x[1];
-          v2 += (float)x[2];
-          v3 += (float)x[3];
+          const uint2 x = *(const uint2 *)(dst + (((wave / K::CG) * K::NT + t) * 32 + r) * K::RS +
+                                           phys_off((wave % K::CG) * K::MT + m, h, g));
+          const f32x2 lo = K::unpk(x.x), hi = K::unpk(x.y);
+          v0 += lo[0];
+          v1 += lo[1];
+          v2 += hi[0];
+          v3 += hi[1];
         }
         acc[m][t][4 * g + 0] = v0;
         acc[m][t][4 * g + 1] = v1;
@@ -243,6 +289,7 @@ __device__ __forceinline__ void acc_init(f32x16 (&acc)[K::MT][K::NT], const char
 template <class K, bool RESID>
 __device__ __forceinline__ void acc_store_bias_relu(const f32x16 (&acc)[K::MT][K::NT], char *dst, const float *bias,
                                                     int wave, int lane) {
+  static_assert(K::BF16, "timing-ablation epilogue: bf16 tiles only");
   const int r = lane & 31, h = lane >> 5;
 #pragma unroll
   for (int m = 0; m < K::MT; ++m)
@@ -273,11 +320,7 @@ __device__ __forceinline__ void acc_store_bias_relu(const f32x16 (&acc)[K::MT][K
 }
 
 // ReLU of a pair as bf16: convert, then a signed 16-bit max with 0 (a negative bf16 is a negative int16).
-__device__ __forceinline__ uint32_t relu_pk_bf16(f32x2 v) {
-  const bf16x2 b = __builtin_convertvector(v, bf16x2);
-  const i16x2 m = __builtin_elementwise_max(__builtin_bit_cast(i16x2, b), i16x2{0, 0});
-  return __builtin_bit_cast(uint32_t, m);
-}
+__device__ __forceinline__ uint32_t relu_pk_bf16(f32x2 v) { return Ty<__bf16>::relu_pk(v); }
 
 // acc_store_bias_relu with the bias already in registers (bv[m][g] = bias[ch(m, g) .. + 4], loaded
 // at the start of the layer so its global-load latency hides under the k-loop instead of stalling
@@ -311,17 +354,17 @@ __device__ __forceinline__ void acc_store_bias_relu_pre(const f32x16 (&acc)[K::M
         float v0 = acc[m][t][4 * g + 0] + bv[m][g].x, v1 = acc[m][t][4 * g + 1] + bv[m][g].y;
         float v2 = acc[m][t][4 * g + 2] + bv[m][g].z, v3 = acc[m][t][4 * g + 3] + bv[m][g].w;
         if constexpr (RESID) {
-          const uint32_t x0 = ((const uint32_t *)&res[t][g >> 1])[2 * (g & 1)];
-          const uint32_t x1 = ((const uint32_t *)&res[t][g >> 1])[2 * (g & 1) + 1];
-          v0 += __uint_as_float(x0 << 16);
-          v1 += __uint_as_float(x0 & 0xffff0000u);
-          v2 += __uint_as_float(x1 << 16);
-          v3 += __uint_as_float(x1 & 0xffff0000u);
+          const f32x2 x0 = K::unpk(((const uint32_t *)&res[t][g >> 1])[2 * (g & 1)]);
+          const f32x2 x1 = K::unpk(((const uint32_t *)&res[t][g >> 1])[2 * (g & 1) + 1]);
+          v0 += x0[0];
+          v1 += x0[1];
+          v2 += x1[0];
+          v3 += x1[1];
         }
-        // ReLU on the converted bf16 pairs (v_cvt_pk_bf16_f32 + v_pk_max_i16: identical bits to
+        // ReLU on the converted pairs (bf16: v_cvt_pk_bf16_f32 + v_pk_max_i16: identical bits to
         // converting max(v, 0), one instruction per pair instead of one per value)
-        o[2 * g] = relu_pk_bf16(f32x2{v0, v1});
-        o[2 * g + 1] = relu_pk_bf16(f32x2{v2, v3});
+        o[2 * g] = K::relu_pk(f32x2{v0, v1});
+        o[2 * g + 1] = K::relu_pk(f32x2{v2, v3});
       }
       *(uint4 *)p = make_uint4(o[0], o[1], o[2], o[3]);
       *(uint4 *)(p + 16) = make_uint4(o[4], o[5], o[6], o[7]);
@@ -336,6 +379,7 @@ __device__ __forceinline__ void acc_store_bias_relu_pre(const f32x16 (&acc)[K::M
 template <class K, bool RESID>
 __device__ __forceinline__ void acc_store_bias_relu_pk(const f32x16 (&acc)[K::MT][K::NT], char *dst, const float *bias,
                                                        int wave, int lane) {
+  static_assert(K::BF16, "timing-ablation epilogue: bf16 tiles only");
   const int r = lane & 31, h = lane >> 5;
 #pragma unroll
   for (int m = 0; m < K::MT; ++m)
@@ -368,12 +412,9 @@ __device__ __forceinline__ void acc_store_relu(const f32x16 (&acc)[K::MT][K::NT]
     for (int g = 0; g < 4; ++g) {
 #pragma unroll
       for (int t = 0; t < K::NT; ++t) {
-        bf16x4 o;
-        o[0] = (__bf16)fmaxf(acc[m][t][4 * g + 0], 0.f);
-        o[1] = (__bf16)fmaxf(acc[m][t][4 * g + 1], 0.f);
-        o[2] = (__bf16)fmaxf(acc[m][t][4 * g + 2], 0.f);
-        o[3] = (__bf16)fmaxf(acc[m][t][4 * g + 3], 0.f);
-        *(bf16x4 *)(dst + (((wave / K::CG) * K::NT + t) * 32 + r) * K::RS + phys_off((wave % K::CG) * K::MT + m, h, g)) = o;
+        const uint2 o = make_uint2(K::relu_pk(f32x2{acc[m][t][4 * g + 0], acc[m][t][4 * g + 1]}),
+                                   K::relu_pk(f32x2{acc[m][t][4 * g + 2], acc[m][t][4 * g + 3]}));
+        *(uint2 *)(dst + (((wave / K::CG) * K::NT + t) * 32 + r) * K::RS + phys_off((wave % K::CG) * K::MT + m, h, g)) = o;
       }
     }
 }
@@ -475,13 +516,13 @@ __device__ __forceinline__ void conv_layer(const char *src, char *dst, const Nbr
         for (int t = 0; t < K::NT; ++t)
 #pragma unroll
           for (int m = 0; m < K::MT; ++m)
-            acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[m], bc[t], f32x16{}, 0, 0, 0);
+            acc[m][t] = K::mfma(acur[m], bc[t], f32x16{});
       } else {
 #pragma unroll
         for (int t = 0; t < K::NT; ++t)
 #pragma unroll
           for (int m = 0; m < K::MT; ++m)
-            acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[m], bc[t], acc[m][t], 0, 0, 0);
+            acc[m][t] = K::mfma(acur[m], bc[t], acc[m][t]);
       }
       if constexpr (!(K::ABL & 256)) {
         // interleave this step's loads (next B fragments, ring refill) between its MFMAs:
@@ -638,13 +679,13 @@ __device__ __forceinline__ void conv_tap_x(const char *src, const Nbr<K> &nb, f3
       for (int t = 0; t < K::NT; ++t)
 #pragma unroll
         for (int m = 0; m < K::MT; ++m)
-          if ((LV >> t) & 1u) acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[m], bc[t], f32x16{}, 0, 0, 0);
+          if ((LV >> t) & 1u) acc[m][t] = K::mfma(acur[m], bc[t], f32x16{});
     } else {
 #pragma unroll
       for (int t = 0; t < K::NT; ++t)
 #pragma unroll
         for (int m = 0; m < K::MT; ++m)
-          if ((LV >> t) & 1u) acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[m], bc[t], acc[m][t], 0, 0, 0);
+          if ((LV >> t) & 1u) acc[m][t] = K::mfma(acur[m], bc[t], acc[m][t]);
     }
 #pragma unroll
     for (int i = 0; i < NTA; ++i) {
@@ -717,13 +758,13 @@ __device__ __forceinline__ void conv_group_x(const char *src, const Nbr<K> &nb, 
         for (int t = 0; t < K::NT; ++t)
 #pragma unroll
           for (int m = 0; m < K::MT; ++m)
-            if ((LV >> t) & 1u) acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[m], bc[t], f32x16{}, 0, 0, 0);
+            if ((LV >> t) & 1u) acc[m][t] = K::mfma(acur[m], bc[t], f32x16{});
       } else {
 #pragma unroll
         for (int t = 0; t < K::NT; ++t)
 #pragma unroll
           for (int m = 0; m < K::MT; ++m)
-            if ((LV >> t) & 1u) acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[m], bc[t], acc[m][t], 0, 0, 0);
+            if ((LV >> t) & 1u) acc[m][t] = K::mfma(acur[m], bc[t], acc[m][t]);
       }
 #pragma unroll
       for (int i = 0; i < NTA; ++i) {
@@ -811,7 +852,7 @@ __device__ __forceinline__ void stem_layer(const char *src, char *dst, const Nbr
       const bf16x8 b = lds_b128(src + nb.off(t, tap) + 16 * h);
 #pragma unroll
       for (int m = 0; m < K::MT; ++m)
-        acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[tap][m], b, acc[m][t], 0, 0, 0);
+        acc[m][t] = K::mfma(a[tap][m], b, acc[m][t]);
     }
   }
   acc_store_relu<K>(acc, dst, wave, lane);
@@ -820,7 +861,7 @@ __device__ __forceinline__ void stem_layer(const char *src, char *dst, const Nbr
 // 1x1 head convs (C -> C/4 policy | C/4 value) + bias + ReLU, to global features
 // [board][cell][C/2] (cell-major: the order the NHWC-reordered linear heads expect).
 template <class K>
-__device__ __forceinline__ void head_layer(const char *src, const bf16x8 *w, const float *bias, __bf16 *out,
+__device__ __forceinline__ void head_layer(const char *src, const bf16x8 *w, const float *bias, uint16_t *out,
                                            int board0, int batch, int wave, int lane) {
   constexpr int KK = K::C / 16;
   constexpr int GROUPS = K::WAVES / K::HCT;  // waves sharing one head channel tile
@@ -851,7 +892,7 @@ __device__ __forceinline__ void head_layer(const char *src, const bf16x8 *w, con
     for (int t = 0; t < TPW; ++t) {
       const int cell = (t0 + t) * 32 + r;
       const bf16x8 b = lds_b128(src + cell * K::RS + koff);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[t], 0, 0, 0);
+      acc[t] = K::mfma(a, b, acc[t]);
     }
   }
   // each lane's output rows, looked up once per cell tile (the row -> board/cell table is read from
@@ -873,12 +914,8 @@ __device__ __forceinline__ void head_layer(const char *src, const bf16x8 *w, con
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
       if (!okr[t]) continue;
-      bf16x4 o;
-      o[0] = (__bf16)fmaxf(acc[t][4 * g + 0] + bv.x, 0.f);
-      o[1] = (__bf16)fmaxf(acc[t][4 * g + 1] + bv.y, 0.f);
-      o[2] = (__bf16)fmaxf(acc[t][4 * g + 2] + bv.z, 0.f);
-      o[3] = (__bf16)fmaxf(acc[t][4 * g + 3] + bv.w, 0.f);
-      *(bf16x4 *)(out + obase[t] + ch) = o;
+      *(uint2 *)(out + obase[t] + ch) = make_uint2(K::relu_pk(f32x2{acc[t][4 * g + 0] + bv.x, acc[t][4 * g + 1] + bv.y}),
+                                                   K::relu_pk(f32x2{acc[t][4 * g + 2] + bv.z, acc[t][4 * g + 3] + bv.w}));
     }
   }
 }
@@ -892,7 +929,7 @@ __device__ __forceinline__ void head_layer(const char *src, const bf16x8 *w, con
 // One workgroup's tile: boards [board0, board0 + BOARDS) of the batch (board < batch), all layers.
 template <class K>
 __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int batch, int board0, int n_blocks,
-                                           const bf16x8 *wpk, const float *bias, __bf16 *out) {
+                                           const bf16x8 *wpk, const float *bias, uint16_t *out) {
   char *X = smem;
   char *Y = smem + K::BUF;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -915,11 +952,11 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
   }
   for (int row = tid; row < K::ROWS; row += K::THREADS) {
     const int board = board0 + K::row_board(row);
-    __bf16 *dst = (__bf16 *)(Y + row * K::RS);
+    uint16_t *dst = (uint16_t *)(Y + row * K::RS);
     const bool ok = row < K::VROWS && board < batch;
     const size_t src = ((size_t)board * K::CELLS + K::row_cell(row)) * 3;
 #pragma unroll
-    for (int c = 0; c < 16; ++c) dst[c] = (ok && c < 3) ? planes[src + c] : (__bf16)0.f;
+    for (int c = 0; c < 16; ++c) dst[c] = (ok && c < 3) ? K::from_bf16(planes[src + c]) : (uint16_t)0;
   }
   __syncthreads();
   nb.finish();
@@ -984,7 +1021,7 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
 
 template <class K>
 __global__ __launch_bounds__(K::THREADS) __attribute__((amdgpu_waves_per_eu(K::WAVES / 4 * K::OCC, K::WAVES / 4 * K::OCC))) void k_tower(
-    const __bf16 *planes, int batch, int n_blocks, const bf16x8 *wpk, const float *bias, __bf16 *out) {
+    const __bf16 *planes, int batch, int n_blocks, const bf16x8 *wpk, const float *bias, uint16_t *out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   tower_tile<K>(smem, planes, batch, blockIdx.x * K::BOARDS, n_blocks, wpk, bias, out);
 }
@@ -1006,7 +1043,7 @@ __host__ __device__ __forceinline__ int tail_kind(int rem, int cus) {
 template <class KF, class KM, class KH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_tower_dyn(
     const __bf16 *planes, const int32_t *count, int max_batch, int cus, int n_blocks, const bf16x8 *wpk,
-    const float *bias, __bf16 *out) {
+    const float *bias, uint16_t *out) {
   static_assert(KF::THREADS == 256 && KM::THREADS == 256 && KH::THREADS == 256, "one block size");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int n = min(*count, max_batch);  // never past the caller's buffers
@@ -1051,8 +1088,8 @@ struct HeadsCfg {
   static_assert(VT % 4 == 0 && FF % 16 == 0 && FROW % 16 == 0, "head tile plan");
 };
 
-template <int FF, int CELLS, int A>
-__global__ __launch_bounds__(256) void k_heads(const __bf16 *feats, int n, const int32_t *count, const bf16x8 *wf,
+template <int FF, int CELLS, int A, class E = __bf16>
+__global__ __launch_bounds__(256) void k_heads(const uint16_t *feats, int n, const int32_t *count, const bf16x8 *wf,
                                                const float *hb, float *probs, float *values) {
   using H = HeadsCfg<FF, CELLS, A>;
   if (count) n = min(*count, n);  // n = the caller's buffer rows
@@ -1107,12 +1144,12 @@ __global__ __launch_bounds__(256) void k_heads(const __bf16 *feats, int n, const
         if (s + D < H::KS) ring[d][v] = wv[((size_t)v * H::KS + s + D) * 64];
       }
 #pragma unroll
-      for (int v = 0; v < H::VTW; ++v) acc[v] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, wcur[v], acc[v], 0, 0, 0);
+      for (int v = 0; v < H::VTW; ++v) acc[v] = Ty<E>::mfma(av, wcur[v], acc[v]);
       if (s >= q0 && s < q1) {
         const bf16x8 ap = *(const bf16x8 *)(frow + (cell * 2 * FF + c) * 2);
         const bf16x8 pw = pnext;
         if (s + 1 < q1) pnext = wp[(size_t)(s + 1) * 64];
-        pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap, pw, pacc, 0, 0, 0);
+        pacc = Ty<E>::mfma(ap, pw, pacc);
       }
     }
   }
@@ -1173,9 +1210,9 @@ __global__ __launch_bounds__(256) void k_heads(const __bf16 *feats, int n, const
 // per workgroup, half the weight traffic of 16), keeps only the cross-wave sums in LDS (4.6 KB), and
 // is held to 96 registers per lane, so one wave fits on each SIMD beside a trunk wave.  Same math
 // in the same order as k_heads (per-wave k order, fixed-order cross-wave sums): bit-identical.
-template <int FF, int CELLS, int A>
+template <int FF, int CELLS, int A, class E = __bf16>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_heads_co(
-    const __bf16 *feats, int n, const int32_t *count, const bf16x8 *wf, const float *hb, float *probs, float *values) {
+    const uint16_t *feats, int n, const int32_t *count, const bf16x8 *wf, const float *hb, float *probs, float *values) {
   using H = HeadsCfg<FF, CELLS, A>;
   constexpr int BOARDS = 32;
   if (count) n = min(*count, n);  // n = the caller's buffer rows
@@ -1223,7 +1260,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         if (s + D < H::KS) ring[d][v] = wv[((size_t)v * H::KS + s + D) * 64];
       }
 #pragma unroll
-      for (int v = 0; v < H::VTW; ++v) acc[v] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, wcur[v], acc[v], 0, 0, 0);
+      for (int v = 0; v < H::VTW; ++v) acc[v] = Ty<E>::mfma(av, wcur[v], acc[v]);
     }
   }
   // value: relu(acc + bv[col]) * wo[col], summed over the hidden units (cols); as k_heads
@@ -1257,7 +1294,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         pn = wp[(size_t)(s + 1) * 64];
         apn = feat(s + 1, 0);
       }
-      pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap, pw, pacc, 0, 0, 0);
+      pacc = Ty<E>::mfma(ap, pw, pacc);
     }
   }
   if (r < A) {
@@ -1328,7 +1365,7 @@ static int launch(const void *planes, int batch, int n_blocks, const void *w, co
     attr_set = true;
   }
   hipLaunchKernelGGL(k_tower<K>, dim3(grid), dim3(K::THREADS), K::LDS, s, (const __bf16 *)planes, batch, n_blocks,
-                     (const bf16x8 *)w, b, (__bf16 *)out);
+                     (const bf16x8 *)w, b, (uint16_t *)out);
   return hipGetLastError() == hipSuccess ? 0 : -11;
 }
 
@@ -1383,10 +1420,36 @@ static int launch_dyn(const void *planes, const int32_t *count, int max_batch, i
     attr_set = true;
   }
   hipLaunchKernelGGL((k_tower_dyn<KF, KM, KH>), dim3(grid), dim3(256), LDS, s, (const __bf16 *)planes, count,
-                     max_batch, cus, n_blocks, (const bf16x8 *)w, b, (__bf16 *)out);
+                     max_batch, cus, n_blocks, (const bf16x8 *)w, b, (uint16_t *)out);
   return hipGetLastError() == hipSuccess ? 0 : -11;
 }
 
+}  // namespace tower
+
+namespace tower {
+// the instantiated tile sets of the device-count path, per board shape, channels and element type
+template <class E>
+static int forward_dev(int32_t width, int32_t height, int32_t channels, int32_t n_blocks, const void *planes_dev,
+                       const int32_t *count_dev, int32_t max_batch, const void *weights_dev, const float *bias_dev,
+                       void *features_dev, bool pack, hipStream_t s) {
+  if (width == 7 && height == 6 && channels == 128)
+    return launch_dyn<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true, true, E>, Cfg<128, 192, 7, 6, 2, 4, 0, 4, 1, false, false, E>,
+                      Cfg<128, 128, 7, 6, 2, 4, 0, 4, 1, false, false, E>>(planes_dev, count_dev, max_batch, n_blocks,
+                                                                          weights_dev, bias_dev, features_dev, pack, s);
+  if (width == 7 && height == 6 && channels == 256)
+    return launch_dyn<Cfg<256, 128, 7, 6, 4, 4, 0, 4, 1, false, false, E>, Cfg<256, 128, 7, 6, 4, 4, 0, 4, 1, false, false, E>,
+                      Cfg<256, 128, 7, 6, 4, 4, 0, 4, 1, false, false, E>>(planes_dev, count_dev, max_batch, n_blocks,
+                                                                          weights_dev, bias_dev, features_dev, pack, s);
+  if (width == 3 && height == 3 && channels == 128)
+    return launch_dyn<Cfg<128, 256, 3, 3, 2, 4, 0, 4, 1, false, false, E>, Cfg<128, 192, 3, 3, 2, 4, 0, 4, 1, false, false, E>,
+                      Cfg<128, 128, 3, 3, 2, 4, 0, 4, 1, false, false, E>>(planes_dev, count_dev, max_batch, n_blocks,
+                                                                          weights_dev, bias_dev, features_dev, pack, s);
+  if (width == 3 && height == 3 && channels == 256)
+    return launch_dyn<Cfg<256, 128, 3, 3, 4, 4, 0, 4, 1, false, false, E>, Cfg<256, 128, 3, 3, 4, 4, 0, 4, 1, false, false, E>,
+                      Cfg<256, 128, 3, 3, 4, 4, 0, 4, 1, false, false, E>>(planes_dev, count_dev, max_batch, n_blocks,
+                                                                          weights_dev, bias_dev, features_dev, pack, s);
+  return -2;
+}
 }  // namespace tower
 
 extern "C" int spmcts_tower_forward_dev(int32_t width, int32_t height, int32_t channels, int32_t n_blocks,
@@ -1395,30 +1458,37 @@ extern "C" int spmcts_tower_forward_dev(int32_t width, int32_t height, int32_t c
                                         int32_t flags, spmcts_stream stream) {
   using namespace tower;
   hipStream_t s = (hipStream_t)stream;
-  if (n_blocks < 0 || max_batch < 0 || !count_dev || (flags & ~SPMCTS_TOWER_PACK)) return -3;
+  if (n_blocks < 0 || max_batch < 0 || !count_dev || (flags & ~(SPMCTS_TOWER_PACK | SPMCTS_TOWER_F16))) return -3;
   if (max_batch == 0) return 0;
   const bool pack = (flags & SPMCTS_TOWER_PACK) != 0;
-  if (width == 7 && height == 6 && channels == 128)
-    return launch_dyn<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true, true>, Cfg<128, 192, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(planes_dev, count_dev, max_batch, n_blocks,
-                                                                      weights_dev, bias_dev, features_dev, pack, s);
-  if (width == 7 && height == 6 && channels == 256)
-    return launch_dyn<Cfg<256, 128, 7, 6, 4>, Cfg<256, 128, 7, 6, 4>, Cfg<256, 128, 7, 6, 4>>(planes_dev, count_dev, max_batch, n_blocks,
-                                                                      weights_dev, bias_dev, features_dev, pack, s);
-  if (width == 3 && height == 3 && channels == 128)
-    return launch_dyn<Cfg<128, 256, 3, 3, 2>, Cfg<128, 192, 3, 3, 2>, Cfg<128, 128, 3, 3, 2>>(planes_dev, count_dev, max_batch, n_blocks,
-                                                                      weights_dev, bias_dev, features_dev, pack, s);
-  if (width == 3 && height == 3 && channels == 256)
-    return launch_dyn<Cfg<256, 128, 3, 3, 4>, Cfg<256, 128, 3, 3, 4>, Cfg<256, 128, 3, 3, 4>>(planes_dev, count_dev, max_batch, n_blocks,
-                                                                      weights_dev, bias_dev, features_dev, pack, s);
-  return -2;
+  if (flags & SPMCTS_TOWER_F16)
+    return forward_dev<_Float16>(width, height, channels, n_blocks, planes_dev, count_dev, max_batch, weights_dev,
+                                 bias_dev, features_dev, pack, s);
+  return forward_dev<__bf16>(width, height, channels, n_blocks, planes_dev, count_dev, max_batch, weights_dev, bias_dev,
+                             features_dev, pack, s);
 }
 
 extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t channels, int32_t n_blocks,
                                     const void *planes_dev, int32_t batch, const void *weights_dev,
-                                    const float *bias_dev, void *features_dev, spmcts_stream stream) {
+                                    const float *bias_dev, void *features_dev, int32_t flags, spmcts_stream stream) {
   using namespace tower;
   hipStream_t s = (hipStream_t)stream;
-  if (n_blocks < 0 || batch < 0) return -3;
+  if (n_blocks < 0 || batch < 0 || (flags & ~SPMCTS_TOWER_F16)) return -3;
+  if (flags & SPMCTS_TOWER_F16) {  // the shipped tile set only (the SPMCTS_TOWER_CG variants are bf16 timing studies)
+    const char *pl = (const char *)planes_dev;
+    char *ft = (char *)features_dev;
+    using E = _Float16;
+    if (width == 7 && height == 6 && channels == 128)
+      return launch_split<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true, true, E>, Cfg<128, 192, 7, 6, 2, 4, 0, 4, 1, false, false, E>,
+                          Cfg<128, 128, 7, 6, 2, 4, 0, 4, 1, false, false, E>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+    if (width == 7 && height == 6 && channels == 256)
+      return launch<Cfg<256, 128, 7, 6, 4, 4, 0, 4, 1, false, false, E>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+    if (width == 3 && height == 3 && channels == 128)
+      return launch<Cfg<128, 256, 3, 3, 2, 4, 0, 4, 1, false, false, E>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+    if (width == 3 && height == 3 && channels == 256)
+      return launch<Cfg<256, 128, 3, 3, 4, 4, 0, 4, 1, false, false, E>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+    return -2;
+  }
   static int cg = -1;
   if (cg < 0) {
     const char *e = getenv("SPMCTS_TOWER_CG");  // A/B switch for the wave split (2 = default)
@@ -1457,6 +1527,7 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
   return -2;
 }
 
+template <class E>
 static int tower_heads(int32_t width, int32_t height, int32_t channels, int32_t actions, const void *features_dev,
                        int32_t batch, const int32_t *count_dev, const void *head_w_dev, const float *head_b_dev,
                        float *probs_dev, float *values_dev, spmcts_stream stream) {
@@ -1469,13 +1540,13 @@ static int tower_heads(int32_t width, int32_t height, int32_t channels, int32_t 
 #define HEADS(FF, CELLS, A)                                                                                   \
   do {                                                                                                        \
   if (co && FF == 32) /* FF = 64 (C = 256) would spill at 96 registers; no room beside that trunk anyway */ \
-    hipLaunchKernelGGL((k_heads_co<FF, CELLS, A>), dim3((batch + 31) / 32), dim3(256), 0, s,                  \
-                       (const __bf16 *)features_dev, batch, count_dev, (const bf16x8 *)head_w_dev, head_b_dev,  \
+    hipLaunchKernelGGL((k_heads_co<FF, CELLS, A, E>), dim3((batch + 31) / 32), dim3(256), 0, s,               \
+                       (const uint16_t *)features_dev, batch, count_dev, (const bf16x8 *)head_w_dev, head_b_dev,\
                        probs_dev, values_dev);                                                                \
   else                                                                                                        \
-    hipLaunchKernelGGL((k_heads<FF, CELLS, A>), dim3((batch + HeadsCfg<FF, CELLS, A>::BOARDS - 1) /           \
+    hipLaunchKernelGGL((k_heads<FF, CELLS, A, E>), dim3((batch + HeadsCfg<FF, CELLS, A>::BOARDS - 1) /        \
                                                      HeadsCfg<FF, CELLS, A>::BOARDS), dim3(256), 0, s,         \
-                         (const __bf16 *)features_dev, batch, count_dev, (const bf16x8 *)head_w_dev, head_b_dev,  \
+                         (const uint16_t *)features_dev, batch, count_dev, (const bf16x8 *)head_w_dev, head_b_dev,\
                        probs_dev, values_dev);                                                                \
   } while (0)
   if (width == 7 && height == 6 && actions == 7 && channels == 128)
@@ -1494,17 +1565,21 @@ static int tower_heads(int32_t width, int32_t height, int32_t channels, int32_t 
 
 extern "C" int spmcts_tower_heads(int32_t width, int32_t height, int32_t channels, int32_t actions,
                                   const void *features_dev, int32_t batch, const void *head_w_dev,
-                                  const float *head_b_dev, float *probs_dev, float *values_dev, spmcts_stream stream) {
-  return tower_heads(width, height, channels, actions, features_dev, batch, nullptr, head_w_dev, head_b_dev, probs_dev,
-                     values_dev, stream);
+                                  const float *head_b_dev, float *probs_dev, float *values_dev, int32_t flags,
+                                  spmcts_stream stream) {
+  if (flags & ~SPMCTS_TOWER_F16) return -3;
+  return (flags & SPMCTS_TOWER_F16 ? tower_heads<_Float16> : tower_heads<__bf16>)(
+      width, height, channels, actions, features_dev, batch, nullptr, head_w_dev, head_b_dev, probs_dev, values_dev, stream);
 }
 
 extern "C" int spmcts_tower_heads_dev(int32_t width, int32_t height, int32_t channels, int32_t actions,
                                       const void *features_dev, const int32_t *count_dev, int32_t max_batch,
                                       const void *head_w_dev, const float *head_b_dev, float *probs_dev,
-                                      float *values_dev, spmcts_stream stream) {
-  return tower_heads(width, height, channels, actions, features_dev, max_batch, count_dev, head_w_dev, head_b_dev,
-                     probs_dev, values_dev, stream);
+                                      float *values_dev, int32_t flags, spmcts_stream stream) {
+  if (flags & ~SPMCTS_TOWER_F16) return -3;
+  return (flags & SPMCTS_TOWER_F16 ? tower_heads<_Float16> : tower_heads<__bf16>)(
+      width, height, channels, actions, features_dev, max_batch, count_dev, head_w_dev, head_b_dev, probs_dev,
+      values_dev, stream);
 }
 
 extern "C" int spmcts_head_epilogue(int32_t hidden, int32_t actions, const void *z_dev, int32_t ldz, int32_t batch,

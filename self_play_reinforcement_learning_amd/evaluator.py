@@ -152,8 +152,9 @@ def make_evaluator(network, game, device=None, dtype=torch.bfloat16, leaf_layout
     if isinstance(network, nn.Module) and hasattr(network, "residual_blocks") and hasattr(network, "conv_policy"):
         if device is not None:
             network.to(device)
-        if backend == "hip" or (backend == "auto" and dtype == torch.bfloat16 and HipTowerEvaluator.supported(network)):
-            return HipTowerEvaluator(network, device=device)
+        if backend == "hip" or (backend == "auto" and dtype in (torch.bfloat16, torch.float16)
+                                and HipTowerEvaluator.supported(network)):
+            return HipTowerEvaluator(network, device=device, dtype=dtype)
         if backend == "auto":
             logging.getLogger(__name__).info(
                 "fused HIP tower not instantiated for %s x %s boards with %d channels (built: 7x6 / 3x3, C = 128 or "
@@ -180,8 +181,8 @@ def phys_channel_order(c):
     return (p - w) + 8 * ((w % 16) // 4) + 4 * (w // 16) + w % 4
 
 
-def _pack_conv(w, cin_pad=None, in_perm=False):
-    """[Cout][Cin][kh][kw] fp -> bf16 fragments [Cout/32][taps][Cin/16][64 lanes][8] (csrc/tower.hip).
+def _pack_conv(w, cin_pad=None, in_perm=False, dtype=torch.bfloat16):
+    """[Cout][Cin][kh][kw] fp -> bf16 / fp16 fragments [Cout/32][taps][Cin/16][64 lanes][8] (csrc/tower.hip).
     in_perm: the layer reads activations another tower layer wrote, which sit in the physical channel
     order (phys_channel_order), so the input-channel axis is permuted to match."""
     cout, cin, kh, kw = w.shape
@@ -194,7 +195,7 @@ def _pack_conv(w, cin_pad=None, in_perm=False):
     w = w.permute(0, 2, 3, 1).reshape(cout, taps, cin)               # [o][tap][c], tap = i*3 + j
     w = w.reshape(cout // 32, 32, taps, cin // 16, 2, 8)             # o = ct*32 + r ; c = kk*16 + h*8 + j
     w = w.permute(0, 2, 3, 4, 1, 5)                                  # [ct][tap][kk][h][r][j] -> lane = h*32 + r
-    return w.reshape(-1).to(torch.bfloat16)
+    return w.reshape(-1).to(dtype)
 
 
 class HipTowerEvaluator(Evaluator):
@@ -202,7 +203,10 @@ class HipTowerEvaluator(Evaluator):
 
     The stem, every BasicBlock and the two 1x1 head convs run in one launch with
     the activations resident in LDS; the three small linear heads (policy
-    1344->A + softmax, value 1344->8ff->1 + tanh) run as bf16 GEMMs in torch.
+    1344->A + softmax, value 1344->8ff->1 + tanh) run in the fused MFMA heads kernel.
+    dtype: the weights' / activations' / head features' element type, torch.bfloat16 or
+    torch.float16 (the reference's inference dtype: amp.autocast, inference_worker.py:117); fp32
+    accumulation, fp32 biases, bf16 0/1 leaf planes either way.
     """
 
     @property
@@ -216,11 +220,15 @@ class HipTowerEvaluator(Evaluator):
     leaf_layout = "nhwc"
     bucket = 1  # the HIP kernels take any batch size; no shape padding needed
 
-    def __init__(self, tower, device=None, fused_heads=True):
+    def __init__(self, tower, device=None, fused_heads=True, dtype=torch.bfloat16):
         """fused_heads: True = MFMA heads kernel (deterministic, batch-independent), "gemm" =
-        one hipBLASLt GEMM + epilogue kernel, False = torch bf16 ops."""
+        one hipBLASLt GEMM + epilogue kernel, False = torch ops in `dtype`."""
         from . import _lib
 
+        if dtype not in (torch.bfloat16, torch.float16):
+            raise ValueError(f"fused tower dtype must be bfloat16 or float16, not {dtype}")
+        self.dtype = dtype
+        self.flags = _lib.TOWER_F16 if dtype == torch.float16 else 0
         self.fused_heads = fused_heads
         self._lib = _lib
         self.tower = tower
@@ -247,16 +255,17 @@ class HipTowerEvaluator(Evaluator):
         fold = InferenceTower._fold
         ws, bs = [], []
         w, b = fold(t.conv1, t.bn1)
-        ws.append(_pack_conv(w, cin_pad=16))
+        dt = self.dtype
+        ws.append(_pack_conv(w, cin_pad=16, dtype=dt))
         bs.append(b)
         for blk in t.residual_blocks:
             for conv, bn in ((blk.conv1, blk.bn1), (blk.conv2, blk.bn2)):
                 w, b = fold(conv, bn)
-                ws.append(_pack_conv(w, in_perm=True))
+                ws.append(_pack_conv(w, in_perm=True, dtype=dt))
                 bs.append(b)
         wp, bp = fold(t.conv_policy, t.policy_bn)
         wv, bv = fold(t.conv_value, t.value_bn)
-        ws.append(_pack_conv(torch.cat([wp, wv], 0), in_perm=True))
+        ws.append(_pack_conv(torch.cat([wp, wv], 0), in_perm=True, dtype=dt))
         bs.append(torch.cat([bp, bv], 0))
         self.n_blocks = len(t.residual_blocks)
         self.wblob = torch.cat(ws).to(dev).contiguous()
@@ -267,7 +276,7 @@ class HipTowerEvaluator(Evaluator):
             m = lin.weight.detach()
             return m.view(m.shape[0], ff, self.W, self.H).permute(0, 2, 3, 1).reshape(m.shape[0], -1)
 
-        bf = torch.bfloat16
+        bf = self.dtype
         self.lp_w = nhwc_cols(t.linear_policy).to(dev, bf).contiguous()
         self.lp_b = t.linear_policy.bias.detach().to(dev, bf)
         self.fv_w = nhwc_cols(t.fc_value).to(dev, bf).contiguous()
@@ -311,7 +320,7 @@ class HipTowerEvaluator(Evaluator):
         """(Re)allocate the device-count path's output buffers for at least `rows` rows."""
         buf = getattr(self, "_dev_bufs", None)
         if buf is None or buf[0].shape[0] < rows or buf[0].device != device:
-            self._dev_bufs = (torch.empty((rows, self.cells, self.C // 2), dtype=torch.bfloat16, device=device),
+            self._dev_bufs = (torch.empty((rows, self.cells, self.C // 2), dtype=self.dtype, device=device),
                               torch.empty((rows, self.A), dtype=torch.float32, device=device),
                               torch.empty(rows, dtype=torch.float32, device=device))
 
@@ -336,7 +345,7 @@ class HipTowerEvaluator(Evaluator):
         timer = getattr(self, "tower_timer", None)
         if timer is not None:
             timer.start()
-        flags = self._lib.TOWER_PACK if self.concurrent else 0
+        flags = (self._lib.TOWER_PACK if self.concurrent else 0) | self.flags
         rc = L.spmcts_tower_forward_dev(self.W, self.H, self.C, self.n_blocks, c(leaves.data_ptr()),
                                         c(count_dev.data_ptr()), max_rows, c(self.wblob.data_ptr()),
                                         c(self.bblob.data_ptr()), c(feats.data_ptr()), flags, stream)
@@ -353,22 +362,22 @@ class HipTowerEvaluator(Evaluator):
         rc = self._lib.lib().spmcts_tower_heads_dev(self.W, self.H, self.C, self.A, c(feats.data_ptr()),
                                                     c(count_dev.data_ptr()), max_rows, c(self.head_w.data_ptr()),
                                                     c(self.head_b.data_ptr()), c(probs.data_ptr()),
-                                                    c(values.data_ptr()), stream)
+                                                    c(values.data_ptr()), self.flags, stream)
         if rc != 0:
             raise self._lib.SpmctsError(f"spmcts_tower_heads_dev failed ({rc})")
         return probs, values
 
     @torch.no_grad()
     def trunk(self, planes_nhwc):
-        """planes: bf16 [n, W, H, 3] contiguous -> head features bf16 [n, cells, C/2]."""
+        """planes: bf16 [n, W, H, 3] contiguous -> head features [n, cells, C/2] in self.dtype."""
         n = planes_nhwc.shape[0]
-        feats = torch.empty((max(n, 1), self.cells, self.C // 2), dtype=torch.bfloat16, device=planes_nhwc.device)
+        feats = torch.empty((max(n, 1), self.cells, self.C // 2), dtype=self.dtype, device=planes_nhwc.device)
         if n:
             stream = torch.cuda.current_stream().cuda_stream
             rc = self._lib.lib().spmcts_tower_forward(
                 self.W, self.H, self.C, self.n_blocks, self._lib.ctypes.c_void_p(planes_nhwc.data_ptr()), n,
                 self._lib.ctypes.c_void_p(self.wblob.data_ptr()), self._lib.ctypes.c_void_p(self.bblob.data_ptr()),
-                self._lib.ctypes.c_void_p(feats.data_ptr()), self._lib.ctypes.c_void_p(stream))
+                self._lib.ctypes.c_void_p(feats.data_ptr()), self.flags, self._lib.ctypes.c_void_p(stream))
             if rc != 0:
                 raise self._lib.SpmctsError(f"spmcts_tower_forward failed ({rc})")
         return feats[:n]
@@ -382,7 +391,7 @@ class HipTowerEvaluator(Evaluator):
         n = planes.shape[0]
         f = self.trunk(planes)
         if self.fused_heads == "gemm":
-            z = torch.matmul(f.reshape(n, -1), self.wc.t())  # one bf16 GEMM for both heads
+            z = torch.matmul(f.reshape(n, -1), self.wc.t()).to(torch.bfloat16)  # one GEMM for both heads
             probs = torch.empty((max(n, 1), self.A), dtype=torch.float32, device=f.device)
             value = torch.empty(max(n, 1), dtype=torch.float32, device=f.device)
             if n:
@@ -400,7 +409,7 @@ class HipTowerEvaluator(Evaluator):
                 c = self._lib.ctypes.c_void_p
                 rc = self._lib.lib().spmcts_tower_heads(
                     self.W, self.H, self.C, self.A, c(f.data_ptr()), n, c(self.head_w.data_ptr()),
-                    c(self.head_b.data_ptr()), c(probs.data_ptr()), c(value.data_ptr()),
+                    c(self.head_b.data_ptr()), c(probs.data_ptr()), c(value.data_ptr()), self.flags,
                     c(torch.cuda.current_stream().cuda_stream))
                 if rc != 0:
                     raise self._lib.SpmctsError(f"spmcts_tower_heads failed ({rc})")

@@ -168,14 +168,14 @@ def _ref_samples(pos):
     return tp, act
 
 
-def _gpu_threaded(opening, N, sims, K, net=None, salt=None):
+def _gpu_threaded(opening, N, sims, K, net=None, salt=None, alpha=1.0):
     """N Philox trees searched from `opening` with K sims in flight (the arena's rolling schedule)."""
     from self_play_reinforcement_learning_amd.arena import Arena, table_net_eval
     from tests.parity_helpers import empty_prior
 
     if net is None:
         arena = Arena("connect4", n_trees=N, iterations=sims, rng="philox", seed=321, leaf_format="f32",
-                      search_threads=K)
+                      search_threads=K, alpha=alpha)
 
         def ev(x):
             return table_net_eval("connect4", x, "f32", "nchw", salt=salt)
@@ -183,7 +183,7 @@ def _gpu_threaded(opening, N, sims, K, net=None, salt=None):
         arena.tree_reset(list(range(N)), [1] * N, priors=np.tile(empty_prior("connect4", salt), (N, 1)))
     else:
         arena = Arena("connect4", n_trees=N, iterations=sims, rng="philox", seed=321, leaf_format=net.leaf_format,
-                      leaf_layout=net.leaf_layout, search_threads=K)
+                      leaf_layout=net.leaf_layout, search_threads=K, alpha=alpha)
         ev = net
         root_p, _ = net(net.empty_root_input(7, 6, arena.device))
         arena.set_root_prior(root_p[0])
@@ -222,7 +222,8 @@ def _close(cp, gp, ca, ga):
 def _resnet_evaluator(d, precision="fp32"):
     """The reference's net (seed-0 init, checked against the fixture's checksums) as the leaf evaluator:
     "fp32" = the PyTorch fp32 forward (BatchNorm folded, TF32 off), so the comparison with the reference's
-    CPU fp32 searches tests the search alone; "bf16" = the fused HIP tower the bench runs."""
+    CPU fp32 searches tests the search alone; "bf16" / "fp16" = the fused HIP tower in that dtype (the
+    bench runs one of them, bench.py --dtype)."""
     from self_play_reinforcement_learning_amd.evaluator import HipTowerEvaluator, TowerEvaluator
     from self_play_reinforcement_learning_amd.modules import ResidualTower
 
@@ -231,8 +232,8 @@ def _resnet_evaluator(d, precision="fp32"):
     sums = {k: float(v.double().sum()) for k, v in net.state_dict().items()}
     for k, v in d["net_checksums"].items():  # the reference's net, bit for bit at init
         assert abs(sums[k] - v) <= 1e-6 * max(1.0, abs(v)), k
-    if precision == "bf16":
-        return HipTowerEvaluator(net.cuda())
+    if precision in ("bf16", "fp16"):
+        return HipTowerEvaluator(net.cuda(), dtype=torch.bfloat16 if precision == "bf16" else torch.float16)
     torch.backends.cudnn.allow_tf32 = False
     torch.backends.cuda.matmul.allow_tf32 = False
     return TowerEvaluator(net.cuda(), dtype=torch.float32, leaf_layout="nchw")
@@ -274,20 +275,50 @@ def test_sequential_search_matches_reference_resnet(pi):
     assert ok, info
 
 
+# Stated bounds on the fused tower's effect on the bench-mode search (K = 4, Philox, 200 sims,
+# ResNet-128x20): every mean visit fraction within TOL of the fp32-evaluator search on the same Philox
+# streams, and within 4.5 SE + TOL of the reference's own threaded samples (G6 resnet_single, 1,000
+# searches per position).  fp16 (the reference's inference dtype) keeps 11 significand bits; bf16 keeps
+# 8 and moves this net's small values (std 0.037) by ~0.002 (scripts/tower_err.py), 8x fp16's error.
+SHIFT_TOL = {"fp16": 0.01, "bf16": 0.03}
+
+
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
 @pytest.mark.parametrize("pi", [0, 1, 2])
-def test_bf16_tower_search_shift(pi):
-    """The bench's bf16 fused tower instead of fp32 leaf evaluation: with this random-init net the
-    values are small (std 0.037) and bf16 moves them by 0.002 on average (scripts/tower_err.py), so the
-    search statistics shift measurably.  Stated bound: every mean visit fraction within 0.03 of the
-    fp32 search's and of the reference's threaded samples (4.5 SE + 0.03)."""
+def test_fused_tower_search_shift(pi, precision):
+    """The bench's fused tower instead of fp32 leaf evaluation, at the stated SHIFT_TOL."""
     d = _g6("resnet_single")
     pos = d["positions"][pi]
-    cp, _ = _ref_samples(pos)
-    fp, _, _ = _gpu_threaded(pos["opening"], 2048, d["sims"], d["thread_count"], net=_resnet_evaluator(d))
-    bp, _, _ = _gpu_threaded(pos["opening"], 2048, d["sims"], d["thread_count"], net=_resnet_evaluator(d, "bf16"))
-    assert (np.abs(bp.mean(0) - fp.mean(0)) <= 0.03).all(), (bp.mean(0).round(4), fp.mean(0).round(4))
+    cp, ca = _ref_samples(pos)
+    assert len(cp) >= 1000
+    tol = SHIFT_TOL[precision]
+    fp, _, _ = _gpu_threaded(pos["opening"], 4096, d["sims"], d["thread_count"], net=_resnet_evaluator(d))
+    bp, ba, _ = _gpu_threaded(pos["opening"], 4096, d["sims"], d["thread_count"], net=_resnet_evaluator(d, precision))
+    assert (np.abs(bp.mean(0) - fp.mean(0)) <= tol).all(), (bp.mean(0).round(4), fp.mean(0).round(4))
     se = np.sqrt(cp.var(0, ddof=1) / len(cp) + bp.var(0, ddof=1) / len(bp))
-    assert (np.abs(bp.mean(0) - cp.mean(0)) <= 4.5 * se + 0.03).all(), (bp.mean(0).round(4), cp.mean(0).round(4))
+    assert (np.abs(bp.mean(0) - cp.mean(0)) <= 4.5 * se + tol).all(), (bp.mean(0).round(4), cp.mean(0).round(4))
+    fc, fg = np.bincount(ca, minlength=7) / len(ca), np.bincount(ba, minlength=7) / len(ba)
+    sef = np.sqrt(fc * (1 - fc) / len(ca) + fg * (1 - fg) / len(ba))
+    assert (np.abs(fc - fg) <= 4.5 * sef + tol).all(), (fc.round(4), fg.round(4))
+
+
+@pytest.mark.parametrize("variant", ["sims100", "alpha0.3"])
+def test_resnet_statistical_check_has_power(variant):
+    """Negative control at the headline net: the fp16-tower comparison at its stated bound (4.5 SE + 0.01)
+    rejects, against the reference's threaded ResNet samples, a search with half the simulation budget
+    (100 instead of 200) and one whose root noise is drawn with Dirichlet alpha 0.3 instead of the
+    reference's 1 (mcts.py:135)."""
+    d = _g6("resnet_single")
+    pos = d["positions"][2]
+    cp, _ = _ref_samples(pos)
+    ev = _resnet_evaluator(d, "fp16")
+    if variant == "sims100":
+        gp, _, _ = _gpu_threaded(pos["opening"], 4096, 100, d["thread_count"], net=ev)
+    else:
+        gp, _, _ = _gpu_threaded(pos["opening"], 4096, d["sims"], d["thread_count"], net=ev, alpha=0.3)
+    se = np.sqrt(cp.var(0, ddof=1) / len(cp) + gp.var(0, ddof=1) / len(gp))
+    assert not (np.abs(gp.mean(0) - cp.mean(0)) <= 4.5 * se + SHIFT_TOL["fp16"]).all(), \
+        (gp.mean(0).round(4), cp.mean(0).round(4), se.round(4))
 
 
 def test_threaded_statistical_check_has_power():

@@ -1,11 +1,12 @@
 """GPU: the fused HIP residual-tower kernel computes the reference network.
 
-Numerics: bf16 MFMA with fp32 accumulation and bf16 activations between layers.
+Numerics: bf16 or fp16 MFMA with fp32 accumulation and bf16 / fp16 activations between layers.
 Tolerance: the fused kernel's deviation from the fp32 reference forward
 (games/general/modules.py:88-107, eval mode) must be within 2x the deviation of
-PyTorch's own bf16 path on the same inputs (+2e-3), and below 0.05 absolute on
-probabilities and values.  Each board is computed independently, so a board's
-output is bit-identical whatever batch it is evaluated in.
+PyTorch's own path in the same dtype on the same inputs (+2e-3; for fp16 that path is
+the reference's own inference mode, torch.autocast fp16, inference_worker.py:117), and
+below 0.05 absolute on probabilities and values.  Each board is computed independently,
+so a board's output is bit-identical whatever batch it is evaluated in.
 """
 import numpy as np
 import pytest
@@ -36,21 +37,26 @@ def _planes(W, H, n, seed=1):
     return planes_from_boards(torch.as_tensor(b), W, H).cuda()
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("game,blocks,ff", [("connect4", 2, 32), ("connect4", 20, 32), ("connect4", 2, 64),
-                                             ("tictactoe", 3, 32)])
-def test_tower_matches_fp32_reference(game, blocks, ff):
+                                             ("connect4", 20, 64), ("tictactoe", 3, 32)])
+def test_tower_matches_fp32_reference(game, blocks, ff, dtype):
     W, H, A = (7, 6, 7) if game == "connect4" else (3, 3, 9)
     net = _net(W, H, A, blocks, ff)
     x = _planes(W, H, 777)
     with torch.no_grad():
         ref_p, ref_v = net.forward_planes(x)
-    hip = HipTowerEvaluator(net)
+    hip = HipTowerEvaluator(net, dtype=dtype)
     xb = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     p, v = hip(xb)
-    tb = TowerEvaluator(net, dtype=torch.bfloat16)
-    p2, v2 = tb(xb)
+    if dtype == torch.float16:  # the reference's inference: fp32 module under fp16 autocast
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
+            p2, v2 = net.forward_planes(x)
+        p2, v2 = p2.float(), v2.float().view(-1)
+    else:
+        p2, v2 = TowerEvaluator(net, dtype=torch.bfloat16)(xb)
     for mode in (False, "gemm"):  # torch heads / GEMM + epilogue heads vs the default MFMA heads kernel
-        p3, v3 = HipTowerEvaluator(net, fused_heads=mode)(xb)
+        p3, v3 = HipTowerEvaluator(net, fused_heads=mode, dtype=dtype)(xb)
         assert (p - p3).abs().max().item() < 1e-2 and (v - v3).abs().max().item() < 1e-2
     e_hip = max((p - ref_p).abs().max().item(), (v - ref_v.view(-1)).abs().max().item())
     e_bf = max((p2 - ref_p).abs().max().item(), (v2 - ref_v.view(-1)).abs().max().item())
@@ -59,9 +65,10 @@ def test_tower_matches_fp32_reference(game, blocks, ff):
     torch.testing.assert_close(p.sum(1), torch.ones(p.shape[0], device=p.device), atol=1e-5, rtol=0)
 
 
-def test_tower_rows_independent_of_batch():
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_tower_rows_independent_of_batch(dtype):
     net = _net(7, 6, 7, 2, 32)
-    hip = HipTowerEvaluator(net)
+    hip = HipTowerEvaluator(net, dtype=dtype)
     x = _planes(7, 6, 1000, seed=5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     full_p, full_v = hip(x)
     for n in (1, 4, 5, 6, 7, 13, 255, 1000):
@@ -72,8 +79,9 @@ def test_tower_rows_independent_of_batch():
     assert torch.equal(p, full_p[3:40]) and torch.equal(v, full_v[3:40])
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("n", [1, 37, 700, 1536, 2336, 4000])
-def test_forward_dev_matches_host_count(n):
+def test_forward_dev_matches_host_count(n, dtype):
     """The device-count launch (row count read on device, full/middle/half workgroups chosen on
     device) gives the host-count results bit for bit on the live rows.  On 256 CUs, 2,336 and 4,000
     rows leave tails of 800 and 928 boards: one round of the 4-board middle tile."""
@@ -81,7 +89,7 @@ def test_forward_dev_matches_host_count(n):
     net = _net(W, H, A, 2, 32)
     max_rows = 4096
     x = _planes(W, H, max_rows, seed=5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    hip = HipTowerEvaluator(net)
+    hip = HipTowerEvaluator(net, dtype=dtype)
     p, v = hip(x[:n].contiguous(memory_format=torch.channels_last))
     cnt = torch.tensor([n], dtype=torch.int32, device=x.device)
     for pack in (False, True):  # round-aligned tiles / SPMCTS_TOWER_PACK (full tiles + one small tail)
@@ -138,16 +146,17 @@ def test_zero_and_maximum_rows():
     assert torch.equal(probs[:64], ref_p) and torch.equal(values[:64].view(-1), ref_v.view(-1))
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("game,n", [("connect4", 1), ("connect4", 31), ("connect4", 33), ("connect4", 1000),
                                     ("connect4", 4096), ("tictactoe", 77)])
-def test_coresident_heads_match_lds_heads(game, n, monkeypatch):
+def test_coresident_heads_match_lds_heads(game, n, dtype, monkeypatch):
     """k_heads_co (features read from global memory, 32 boards per workgroup, 96 registers: fits beside
     a trunk workgroup) gives the LDS-staged k_heads' results bit for bit: same per-wave k order, same
     fixed-order cross-wave sums; ragged tails (n % 32) read only live boards."""
     W, H, A = (7, 6, 7) if game == "connect4" else (3, 3, 9)
     net = _net(W, H, A, 2, 32)
     x = _planes(W, H, n, seed=11).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    hip = HipTowerEvaluator(net)
+    hip = HipTowerEvaluator(net, dtype=dtype)
     monkeypatch.setenv("SPMCTS_HEADS", "lds")
     p0, v0 = hip(x)
     torch.cuda.synchronize()
@@ -156,3 +165,23 @@ def test_coresident_heads_match_lds_heads(game, n, monkeypatch):
     torch.cuda.synchronize()
     assert torch.equal(p0, p1) and torch.equal(v0, v1)
     assert torch.isfinite(p1).all() and torch.isfinite(v1).all()
+
+
+@pytest.mark.parametrize("ff", [32, 64])
+def test_fp16_bench_nets_finite_and_close(ff):
+    """The bench's nets as the bench builds them (ResidualTower(7, 6, 7, 20 blocks, filter_factor 32 /
+    64), seed-0 default init, BatchNorm at its init statistics) in the fp16 tower: every output finite
+    (no activation overflow in fp16; tests/test_fp16_range.py bounds the activations on the host) and
+    within 2x torch fp16 autocast's deviation from the fp32 forward (+2e-3)."""
+    torch.manual_seed(0)
+    net = ResidualTower(7, 6, 7, num_blocks=20, filter_factor=ff).cuda().eval()
+    x = _planes(7, 6, 2048, seed=3)
+    with torch.no_grad():
+        ref_p, ref_v = net.forward_planes(x)
+        with torch.autocast("cuda", dtype=torch.float16):
+            ap, av = net.forward_planes(x)
+    p, v = HipTowerEvaluator(net, dtype=torch.float16)(x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+    assert torch.isfinite(p).all() and torch.isfinite(v).all()
+    e_hip = max((p - ref_p).abs().max().item(), (v - ref_v.view(-1)).abs().max().item())
+    e_ac = max((ap.float() - ref_p).abs().max().item(), (av.float() - ref_v).abs().max().item())
+    assert e_hip <= 2 * e_ac + 2e-3, (e_hip, e_ac)
