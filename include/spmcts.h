@@ -168,6 +168,14 @@ int spmcts_expand2(spmcts_arena *h, const float *probs0_dev, const float *values
  * spmcts_player_kind; budgets = simulations per search (MCTreeSearch.iterations of that
  * player; < 0 = unlimited).  Network-1 leaves are placed from row seg1 = #network-0 trees. */
 int spmcts_set_tree_players(spmcts_arena *h, const uint8_t *nets, const uint8_t *kinds, const int32_t *budgets);
+/* (sync) Per-tree search settings: each side of an evaluation game searches with its own
+ * MCTreeSearch kwargs (selfplayworker.py:71-81 builds the opponent from its own container;
+ * mcts.py:119-136): alpha = Dirichlet alpha of the root noise (mcts.py:49-53, > 0),
+ * strong_play = terminal-value shaping (mcts.py:305-311), search_threads = sims in flight
+ * (thread_count, mcts.py:328-331; 1 .. the arena's search_threads).  Host arrays of n_trees
+ * entries; NULL = unchanged (defaults: the arena config's values). */
+int spmcts_set_tree_search(spmcts_arena *h, const double *alpha, const uint8_t *strong_play,
+                           const int32_t *search_threads);
 int spmcts_arena_segments(const spmcts_arena *h, int32_t *seg1);
 /* Empty-board root prior of network `net` (0 / 1), used by resets of that network's trees. */
 int spmcts_set_root_prior_net(spmcts_arena *h, int32_t net, const float *probs_dev, spmcts_stream stream);

@@ -14,7 +14,8 @@ from .mcts import OracleTree
 
 def play_episode(game, net_policy, net_opponent, rng_policy, rng_opponent, iterations, swap_sides=False,
                  update=True, evaluate=False, alpha=1, strong_play=False, on_ply=None, opponent="mcts",
-                 opponent_iterations=None, threads=1):
+                 opponent_iterations=None, threads=1, opponent_alpha=None, opponent_strong_play=None,
+                 opponent_threads=None):
     """SelfPlayer.play_episode (selfplayworker.py:172-194).
 
     The reference draws every random number from ONE global RandomState, in
@@ -29,6 +30,8 @@ def play_episode(game, net_policy, net_opponent, rng_policy, rng_opponent, itera
     push order [policy's then opponent's], per-ply log).
 
     threads=K > 1: both trees search with K sims in flight (oracle/mcts.py threaded mode).
+    opponent_alpha / opponent_strong_play / opponent_threads: the opposing MCTreeSearch's own kwargs
+    (selfplayworker.py:71-81 builds it from its own container); None = the policy's.
     """
     env = make_env(game)
     env.reset()
@@ -36,8 +39,11 @@ def play_episode(game, net_policy, net_opponent, rng_policy, rng_opponent, itera
                      root_player=(-1 if swap_sides else 1), threads=threads)
     if opponent == "mcts":
         opp = OracleTree(game, net_opponent, rng_opponent,
-                         iterations if opponent_iterations is None else opponent_iterations, alpha, strong_play,
-                         evaluate=evaluate, root_player=(1 if swap_sides else -1), threads=threads)
+                         iterations if opponent_iterations is None else opponent_iterations,
+                         alpha if opponent_alpha is None else opponent_alpha,
+                         strong_play if opponent_strong_play is None else opponent_strong_play,
+                         evaluate=evaluate, root_player=(1 if swap_sides else -1),
+                         threads=threads if opponent_threads is None else opponent_threads)
     else:
         opp = HardcodedPlayer(opponent, game, rng_opponent)
         opp.reset(1 if swap_sides else -1)

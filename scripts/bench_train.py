@@ -1,0 +1,77 @@
+"""train_model throughput: self-play positions/s with the trainer on (SelfPlayScheduler's own loop:
+`updates_per_ply` AZ-loss SGD steps queued after every ply, updateworker.py:141-149), plus SGD steps/s.
+
+Workload: BASELINE configs[1] (Connect4, 200 sims, 4,096 games, ResNet-128x20, K = 4, two lanes) with
+the reference's trainer settings (batch 64, SGD lr 0.001 momentum 0.9 wd 1e-4, min_memory 20,000,
+memory 200,000).  The replay ring is first filled past min_memory (untimed), then --plies plies are
+timed with the trainer stepping, with its steps on their own stream (overlap, the default) or on the
+arena's stream (--no-overlap), and once with updates_per_ply = 0 for the self-play-only rate.
+
+    python scripts/bench_train.py [--plies 24] [--updates 4]   -> one JSON line
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def run(args, updates, overlap):
+    import torch
+
+    from self_play_reinforcement_learning_amd import Connect4Env, MCTreeSearch, ModelContainer, SelfPlayScheduler
+    from self_play_reinforcement_learning_amd.modules import ResidualTower
+
+    torch.manual_seed(0)
+    net = ResidualTower(7, 6, 7, num_blocks=20, filter_factor=32).cuda()
+    kw = dict(iterations=args.sims, env=Connect4Env, batch_size=64, memory_size=200000, min_memory=args.min_memory)
+    sp = SelfPlayScheduler(ModelContainer(MCTreeSearch, policy_kwargs=kw), Connect4Env, network=net, save_dir=None,
+                           n_games=args.games, updates_per_ply=updates, overlap_training=overlap, evaluation_games=0,
+                           lr=0.001)
+    sp.setup_player_workers()
+    sp.setup_update_worker()
+    eng, tr = sp.engine, sp.trainer
+    on_moves, on_ply = sp._callbacks(update=True)
+    eng.start()
+    fill_plies = 0
+    while len(tr.memory) < args.min_memory + 1000:  # untimed: the ring past min_memory (trainer starts)
+        eng.ply(on_moves=on_moves)
+        fill_plies += 1
+    for _ in range(2):  # warm the trainer's kernels
+        eng.ply(on_moves=on_moves)
+        on_ply(eng)
+    tr.sync()
+    torch.cuda.synchronize()
+    m0, s0 = eng.counters()["moves"], tr.steps
+    t0 = time.perf_counter()
+    for _ in range(args.plies):
+        eng.ply(on_moves=on_moves)
+        on_ply(eng)
+    tr.sync()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    moves, steps = eng.counters()["moves"] - m0, tr.steps - s0
+    loss = float(tr.last_loss) if tr.last_loss is not None else None
+    return dict(updates_per_ply=updates, trainer_stream=overlap, plies=args.plies, seconds=dt,
+                positions_per_s=moves / dt, sgd_steps=steps, sgd_steps_per_s=steps / dt, fill_plies=fill_plies,
+                replay_rows=len(tr.memory), last_loss=loss)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--plies", type=int, default=24)
+    ap.add_argument("--updates", type=int, default=4)
+    ap.add_argument("--games", type=int, default=4096)
+    ap.add_argument("--sims", type=int, default=200)
+    ap.add_argument("--min-memory", type=int, default=20000)
+    args = ap.parse_args()
+    out = dict(workload=f"connect4 self-play + training, {args.sims} sims, {args.games} games, ResNet-128x20 (bf16 "
+                        f"trunk for leaves, fp32 SGD batch 64), K = 4, two lanes",
+               runs=[run(args, args.updates, True), run(args, args.updates, False), run(args, 0, True)])
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

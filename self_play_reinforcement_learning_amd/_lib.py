@@ -101,6 +101,7 @@ _SIGS = {
     "spmcts_expand": [_P, _P, _P, _P],
     "spmcts_expand2": [_P, _P, _P, _P, _P, _P],
     "spmcts_set_tree_players": [_P, _P, _P, _P],
+    "spmcts_set_tree_search": [_P, _P, _P, _P],
     "spmcts_arena_segments": [_P, ctypes.POINTER(_I32)],
     "spmcts_set_root_prior_net": [_P, _I32, _P, _P],
     "spmcts_games_set_record": [_P, _I32],

@@ -178,6 +178,29 @@ class Arena:
         call("spmcts_arena_segments", self.h, ctypes.byref(seg))
         self.seg1 = seg.value
 
+    def set_tree_search(self, alpha=None, strong_play=None, search_threads=None):
+        """Per-tree search settings (include/spmcts.h spmcts_set_tree_search): each side of an
+        evaluation game searches with its own MCTreeSearch kwargs (selfplayworker.py:71-81):
+        Dirichlet alpha, strong_play, sims in flight (1 .. this arena's search_threads).  None =
+        unchanged."""
+        T = self.n_trees
+
+        def arr(x, ctype, dtype):
+            if x is None:
+                return None
+            a = np.ascontiguousarray(np.asarray(x, dtype=dtype))
+            if a.shape != (T,):
+                raise ValueError(f"expected {T} per-tree entries, got {a.shape}")
+            return a.ctypes.data_as(ctypes.POINTER(ctype)), a
+
+        al = arr(alpha, ctypes.c_double, np.float64)
+        st = arr(strong_play, ctypes.c_uint8, np.uint8)
+        k = arr(search_threads, ctypes.c_int32, np.int32)
+        torch.cuda.current_stream().synchronize()
+        call("spmcts_set_tree_search", self.h, al[0] if al else None, st[0] if st else None, k[0] if k else None)
+        if search_threads is not None:
+            self.tree_threads = np.asarray(search_threads, dtype=np.int64)
+
     def games_set_record(self, record=True):
         call("spmcts_games_set_record", self.h, int(bool(record)))
 

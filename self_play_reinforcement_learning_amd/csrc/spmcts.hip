@@ -154,6 +154,11 @@ struct View {
   uint8_t *tnet;     // [T] network whose leaves this tree sends (0 / 1)
   uint8_t *tkind;    // [T] SPMCTS_PLAYER_*: MCTS, or a hard-coded player (hardcoded_players.py)
   int32_t *budget;   // [T] simulations per search of this tree (MCTreeSearch.iterations)
+  // per-tree search settings (each side of an evaluation game is built from its own container's
+  // kwargs, selfplayworker.py:71-81): Dirichlet alpha, strong_play, sims in flight (<= K)
+  double *talpha;
+  uint8_t *tstrong;
+  int32_t *tK;
   int32_t seg1;      // first leaf row of network 1 (= number of network-0 trees)
   int32_t record;    // games mode: keep Move records (play_episode update=True)
   int32_t sim;       // index of the current simulation within the search (by value per launch)
@@ -294,9 +299,9 @@ __device__ __forceinline__ void reset_tree(const View &v, int tree, int player, 
   for (int j = 0; j < v.K; ++j) v.need[(size_t)tree * v.K + j] = 0;
 }
 
-// terminal value of _expand_node (mcts.py:305-313); r = reward * mover
-__device__ __forceinline__ double terminal_value(const View &v, Board parent, int r) {
-  if (v.strong) {
+// terminal value of _expand_node (mcts.py:305-313) for `tree`'s own strong_play; r = reward * mover
+__device__ __forceinline__ double terminal_value(const View &v, int tree, Board parent, int r) {
+  if (v.tstrong[tree]) {
     const int num_steps = popc(parent.pos | parent.neg) + 1;  // np.sum(np.abs(state)) + 1
     return (1.18 - ((double)(9 * num_steps) / 350.0)) * (double)r;
   }
@@ -321,7 +326,7 @@ __device__ void draw_noise(const View &v, int tree) {
     Philox st = v.rng[tree];
     double acc = 0.0;
     for (int j = 0; j < G::A; ++j) {
-      g[j] = gamma_draw(&st, v.alpha);
+      g[j] = gamma_draw(&st, v.talpha[tree]);
       acc += g[j];
     }
     const double inv = acc > 0.0 ? 1.0 / acc : 0.0;
@@ -623,16 +628,17 @@ __global__ __launch_bounds__(64) void k_select(View v, int n_active) {
         cnt[C_DEPTH] += depth + 1;
         if (done) {
           // terminal: value r (or strong_play shaping), no children, backup in place
-          const double val = terminal_value(v, b, rew * player);
+          const double val = terminal_value(v, tree, b, rew * player);
+          const bool strong = v.tstrong[tree] != 0;
           for (int k = 0; k <= depth; ++k) {
             const size_t idx = nb + s_node[grp][k];
             v.bn[idx] = s_n[grp][k] + 1;
             v.bw[idx] = s_w[grp][k] + val;
-            if (v.strong) v.bf64[idx] = 1;
+            if (strong) v.bf64[idx] = 1;
           }
           v.bn[nb + child] = cn_a + 1;
           v.bw[nb + child] = cw_a + val;
-          if (v.strong) v.bf64[nb + child] = 1;
+          if (strong) v.bf64[nb + child] = 1;
           cnt[C_TERM] += 1;
         } else {
           // pending network evaluation: stash the path for k_expand
@@ -793,18 +799,19 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
       if (done) {
         // terminal: backup (mcts.py:94-98) then remove the path's virtual loss (:365); one lane per
         // path node (s_node was written by lane 0 of this wave: LDS operations of a wave stay in order)
-        const double val = terminal_value(v, b, rew * player);
+        const double val = terminal_value(v, tree, b, rew * player);
+        const bool strong = v.tstrong[tree] != 0;
         for (int k = lane; k <= depth; k += P) {
           const size_t idx = nb + s_node[k];
           v.bn[idx] += 1;
           v.bw[idx] += val;
-          if (v.strong) v.bf64[idx] = 1;
+          if (strong) v.bf64[idx] = 1;
           v.bvl[idx] -= 1;
         }
         if (lane == 0) {
           v.bn[nb + child] += 1;
           v.bw[nb + child] += val;
-          if (v.strong) v.bf64[nb + child] = 1;
+          if (strong) v.bf64[nb + child] = 1;
         }
         R.n += 1;  // the root is s_node[0]
         R.vl -= 1;
@@ -883,7 +890,8 @@ __global__ __launch_bounds__(TB) void k_select_vl(View v, int n_active) {
   TreeRoot R = load_root<G>(v, tree);
   bool terr = false;
   int64_t *cnt = v.cnt + (size_t)tree * C_NCNT;
-  for (int j = 0; j < v.K; ++j) {
+  const int kt = v.tK[tree];  // this tree's sims in flight (its own thread_count, <= K)
+  for (int j = 0; j < kt; ++j) {
     if (v.need[tree * v.K + j]) continue;
     if (fill_slot_vl<G>(v, tree, j, limit, started, R, rng, terr, s_node[grp], noise, nz, cnt) == SIM_ERROR) return;
   }
@@ -1413,10 +1421,10 @@ __device__ bool set_node(const View &v, int tree, int a) {
     int64_t *cnt = v.cnt + (size_t)tree * C_NCNT;
     cnt[C_SETNODE] += 1;
     if (done) {
-      const double val = terminal_value(v, Board{v.rpos[tree], v.rneg[tree]}, rew * rp);
+      const double val = terminal_value(v, tree, Board{v.rpos[tree], v.rneg[tree]}, rew * rp);
       v.bn[nb + child] = 1;
       v.bw[nb + child] = v.bw[nb + child] + val;
-      if (v.strong) v.bf64[nb + child] = 1;
+      if (v.tstrong[tree]) v.bf64[nb + child] = 1;
     } else {
       const int ps = tree * v.K;  // pending slot 0 of the tree
       v.plen[ps] = 0;
@@ -1906,6 +1914,9 @@ static void plan_arena(spmcts_arena *h, Plan &pl) {
   pl.add(&v.tnet, T);
   pl.add(&v.tkind, T);
   pl.add(&v.budget, T);
+  pl.add(&v.talpha, T);
+  pl.add(&v.tstrong, T);
+  pl.add(&v.tK, T);
 }
 
 static int setup_view(spmcts_arena *h, const spmcts_config *cfg) {
@@ -1964,6 +1975,9 @@ __global__ void k_rng_init(View v, uint64_t seed, uint64_t sub0) {
   v.tnet[t] = 0;
   v.tkind[t] = SPMCTS_PLAYER_MCTS;
   v.budget[t] = 0x7fffffff;
+  v.talpha[t] = v.alpha;
+  v.tstrong[t] = (uint8_t)(v.strong ? 1 : 0);
+  v.tK[t] = v.K;
   for (int k = 0; k < C_NCNT; ++k) v.cnt[(size_t)t * C_NCNT + k] = 0;
 }
 
@@ -2251,6 +2265,30 @@ int spmcts_set_tree_players(spmcts_arena *h, const uint8_t *nets, const uint8_t 
   HIP_TRY(hipMemcpy(h->v.tkind, kd.data(), T, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(h->v.budget, bd.data(), 4 * (size_t)T, hipMemcpyHostToDevice));
   h->v.seg1 = n0 * h->v.K;  // network-0 trees never have more than n0 * K pending leaves
+  return 0;
+}
+
+int spmcts_set_tree_search(spmcts_arena *h, const double *alpha, const uint8_t *strong_play,
+                           const int32_t *search_threads) {
+  if (!h) return fail(-1, "null arena");
+  const int T = h->v.T;
+  if (alpha) {
+    for (int t = 0; t < T; ++t)
+      if (!(alpha[t] > 0.0)) return fail(-3, "alpha must be > 0");
+  }
+  if (search_threads) {
+    for (int t = 0; t < T; ++t)
+      if (search_threads[t] < 1 || search_threads[t] > h->v.K)
+        return fail(-3, "per-tree search_threads must be in [1, the arena's search_threads]");
+  }
+  HIP_TRY(hipDeviceSynchronize());
+  if (alpha) HIP_TRY(hipMemcpy(h->v.talpha, alpha, sizeof(double) * (size_t)T, hipMemcpyHostToDevice));
+  if (strong_play) {
+    std::vector<uint8_t> st(T);
+    for (int t = 0; t < T; ++t) st[t] = strong_play[t] ? 1 : 0;
+    HIP_TRY(hipMemcpy(h->v.tstrong, st.data(), (size_t)T, hipMemcpyHostToDevice));
+  }
+  if (search_threads) HIP_TRY(hipMemcpy(h->v.tK, search_threads, 4 * (size_t)T, hipMemcpyHostToDevice));
   return 0;
 }
 

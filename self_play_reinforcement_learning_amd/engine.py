@@ -87,7 +87,11 @@ class SelfPlayEngine:
     def __init__(self, game, network, n_games=4096, iterations=200, alpha=1.0, strong_play=False, evaluate=False,
                  seed=0, subsequence0=None, rng="philox", max_games=None, device=None, dtype=torch.bfloat16,
                  leaf_layout="nhwc", cpuct=4.0, x_noise=0.25, blocks_per_tree=0, bucket=256, opponent=None,
-                 opponent_iterations=None, record=True, search_threads=1, leaf_dedup=None):
+                 opponent_iterations=None, record=True, search_threads=1, leaf_dedup=None, opponent_alpha=None,
+                 opponent_strong_play=None, opponent_search_threads=None):
+        """opponent_alpha / opponent_strong_play / opponent_search_threads: the opposing MCTS side's own
+        search settings (evaluation games: each side is built from its own container's kwargs,
+        selfplayworker.py:71-81); None = the policy's."""
         self.game = game
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.evaluator = make_evaluator(network, game, device=self.device, dtype=dtype, leaf_layout=leaf_layout)
@@ -108,6 +112,10 @@ class SelfPlayEngine:
                                  f"({e0.leaf_format}/{e0.leaf_layout} vs {e1.leaf_format}/{e1.leaf_layout})")
         it1 = iterations if opponent_iterations is None else int(opponent_iterations)
         self.iterations = max(iterations, it1) if opp_kind == _lib.PLAYER_MCTS else iterations
+        k0 = max(1, int(search_threads))
+        k1 = k0 if opponent_search_threads is None or opp_kind != _lib.PLAYER_MCTS else max(1, int(opponent_search_threads))
+        a1 = alpha if opponent_alpha is None else float(opponent_alpha)
+        s1 = strong_play if opponent_strong_play is None else bool(opponent_strong_play)
         rank = distributed.env_rank()[0]
         if subsequence0 is None:
             subsequence0 = rank * 2 * n_games  # disjoint Philox subsequences per rank
@@ -115,10 +123,17 @@ class SelfPlayEngine:
                            seed=seed, subsequence0=subsequence0, strong_play=strong_play, evaluate=evaluate,
                            leaf_format=self.evaluator.leaf_format, leaf_layout=self.evaluator.leaf_layout,
                            cpuct=cpuct, x_noise=x_noise, alpha=alpha, blocks_per_tree=blocks_per_tree,
-                           device=self.device, search_threads=search_threads)
-        # K sims in flight per tree (the reference's thread_count search, mcts.py:328-331)
+                           device=self.device, search_threads=max(k0, k1))
+        # K sims in flight per tree (the reference's thread_count search, mcts.py:328-331); a search of
+        # `budget` sims with k in flight takes ceil(budget / k) network steps
         self.search_threads = self.arena.search_threads
-        self.select_steps = -(-self.iterations // self.search_threads)
+        self.select_steps = -(-iterations // k0)
+        if opp_kind == _lib.PLAYER_MCTS:
+            self.select_steps = max(self.select_steps, -(-it1 // k1))
+        if (k1, a1, s1) != (k0, alpha, strong_play) or k0 != self.search_threads:
+            # tree 2g = the policy, 2g + 1 = the opposing player, each with its own kwargs
+            self.arena.set_tree_search(alpha=[alpha, a1] * n_games, strong_play=[strong_play, s1] * n_games,
+                                       search_threads=[k0, k1] * n_games)
         if self.evaluator1 is not None or opp_kind != _lib.PLAYER_MCTS or it1 != iterations:
             # tree 2g = the policy, 2g + 1 = the opposing player (selfplayworker.py:164-176)
             self.arena.set_tree_players(nets=[0, 1 if self.evaluator1 is not None else 0] * n_games,

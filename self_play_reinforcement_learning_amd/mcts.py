@@ -110,6 +110,9 @@ class MCTreeSearch(Policy):
                             device=self.device, search_threads=k)
         self.temp_memory = []
         self.moves_played = 0
+        # weights changed (update_from_memory / load_state_dict): the evaluator's folded / packed copy is
+        # refreshed before the next leaf evaluation, the empty-board root prior at the next reset
+        self._weights_stale = False
         self._root_prior_stale = True
         if starting_state_dict:
             self.load_state_dict(starting_state_dict)
@@ -117,9 +120,16 @@ class MCTreeSearch(Policy):
         self.reset()
 
     # ------------------------------------------------------------------ search
+    def _sync_weights(self):
+        """The reference evaluates every leaf with the network as it is now (mcts.py:316): after an
+        update the evaluator's packed weights are re-derived before the next evaluation."""
+        if self._weights_stale:
+            if hasattr(self._evaluator, "refresh"):
+                self._evaluator.refresh()
+            self._weights_stale = False
+
     def _refresh_root_prior(self):
-        if hasattr(self._evaluator, "refresh"):
-            self._evaluator.refresh()
+        self._sync_weights()
         x = self._evaluator.empty_root_input(self.W, self.H, self.device)
         probs, _ = self._evaluator(x)
         self._arena.set_root_prior(probs[0])
@@ -127,6 +137,7 @@ class MCTreeSearch(Policy):
 
     def _eval_expand(self, n):
         if n:
+            self._sync_weights()
             probs, values = self._evaluator(self._arena.leaves(n))
             self._arena.expand(probs, values)
 
@@ -209,6 +220,7 @@ class MCTreeSearch(Policy):
         self.optim.zero_grad()
         loss.backward()
         self.optim.step()
+        self._weights_stale = True
         self._root_prior_stale = True
 
     @property
@@ -217,6 +229,7 @@ class MCTreeSearch(Policy):
 
     def load_state_dict(self, state_dict, target=False):
         self.network.load_state_dict(state_dict)
+        self._weights_stale = True
         self._root_prior_stale = True
 
     def state_dict(self):

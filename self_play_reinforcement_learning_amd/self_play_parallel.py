@@ -92,7 +92,7 @@ class SelfPlayScheduler:
                  save_dir="saves", epoch_length=500, initial_games=64, lr=0.001, stagger=False, evaluation_games=100,
                  evaluation_network=None, stagger_mem_step=5000, deduplicate=False, update_delay=0.01,
                  self_play=None, n_games=None, device=None, seed=0, updates_per_ply=4, lanes=None, exchange_every=8,
-                 gpus=None, start_time=None):
+                 gpus=None, start_time=None, overlap_training=True):
         # constructor arguments, for rank processes started by this scheduler (_run_ranks)
         self._init_kwargs = {k: v for k, v in locals().items() if k not in ("self", "__class__")}
         self.policy_container = policy_container
@@ -114,6 +114,8 @@ class SelfPlayScheduler:
         self.network = self._get_network(network, policy_container)
         self.seed = seed
         self.updates_per_ply = updates_per_ply
+        # the trainer's SGD steps on a HIP stream of their own, beside the arena's plies (_Trainer)
+        self.overlap_training = overlap_training
         self.exchange_every = exchange_every  # plies per episode-batch exchange round (distributed.MoveExchange)
         # >1: LanedEngine (arenas on separate HIP streams, each a complete arena); None = 2 lanes for
         # arenas of >= 1,024 games, where the overlap pays (bench.py), else one arena
@@ -132,7 +134,7 @@ class SelfPlayScheduler:
         self.engine = None
         self.trainer = None
         self.epoch_value = 0
-        self._search_threads = 1
+        self._search_threads = self._opponent_threads = 1
         if policy_container is not None:
             self._resolve_threads(True)  # the default of every entry point (inference_proxy=True)
         if save_dir and rank == 0:
@@ -159,15 +161,15 @@ class SelfPlayScheduler:
         """Simulations in flight per tree, resolved in one place for self-play and evaluation
         games: the reference's workers search with thread_count threads + virtual loss exactly when
         they talk to an InferenceProxy (mcts.py:154, self_play_parallel.py:95-171), which every
-        scheduler entry point does by default.  One arena holds both players, so an evaluation
-        opponent with another thread_count is searched with the policy's (logged)."""
-        k = max(1, int(self._policy_kwargs().get("thread_count", 4) or 1)) if inference_proxy else 1
-        c = self.evaluation_policy_container
-        okw = getattr(c, "policy_kwargs", None) or {}
-        if inference_proxy and c is not None and "thread_count" in okw and max(1, int(okw["thread_count"] or 1)) != k:
-            logging.warning(f"evaluation policy thread_count={okw['thread_count']} differs from the policy's "
-                            f"{k}; the arena searches both sides with {k} simulations in flight")
+        scheduler entry point does by default.  The evaluation opponent is built from its own
+        container's kwargs (selfplayworker.py:71-81), so it searches with its own thread_count."""
+        def threads(kw):
+            return max(1, int(kw.get("thread_count", 4) or 1)) if inference_proxy else 1
+
+        k = threads(self._policy_kwargs())
+        okw = getattr(self.evaluation_policy_container, "policy_kwargs", None) or {}
         self._search_threads = k
+        self._opponent_threads = threads(okw)
         return k
 
     def setup_player_workers(self, num_workers=None, inference_proxy=True, threads_per_worker=8, resume_model=False):
@@ -195,7 +197,7 @@ class SelfPlayScheduler:
         self.trainer = _Trainer(self.network, optim, memory_size=kw.get("memory_size", 200000),
                                 batch_size=kw.get("batch_size", 64), min_memory=kw.get("min_memory", 20000),
                                 q_average=kw.get("q_average", True), device=self.device, W=self.W, H=self.H,
-                                A=self.A)
+                                A=self.A, overlap=self.overlap_training)
         if resume_model:
             self._load_latest(prev_run=True)
         return self.trainer, None, None
@@ -226,10 +228,18 @@ class SelfPlayScheduler:
         self_play_parallel.py:236-238); Moves -> memory_queue (rank 0), results -> result_queue."""
         eng = self.engine
         per_rank = n_games // self.world + (1 if self.rank < n_games % self.world else 0)
+        on_moves, on_ply = self._callbacks(update)
+        eng.play_games(per_rank, on_moves=on_moves, on_ply=on_ply, every=self.exchange_every)
+        eng.check()
+
+    def _callbacks(self, update=True):
+        """(on_moves, on_ply) of a self-play run: gathered Move rows into the replay ring (rank 0) and
+        the results queue; `updates_per_ply` trainer steps queued after every ply."""
 
         def on_moves(g):
             # rank 0 (the replay owner): a batch of Move rows gathered from every rank (MoveExchange)
             if update and self.trainer is not None:
+                self.trainer.sync()  # queued SGD steps sample the ring: they finish before rows are overwritten
                 self.trainer.memory.add_moves(g)  # device replay ring: no per-record host objects
             elif update:
                 for rec in moves_to_records(g, self.W, self.H):
@@ -246,8 +256,7 @@ class SelfPlayScheduler:
                 for _ in range(self.updates_per_ply):
                     self.trainer.step()
 
-        eng.play_games(per_rank, on_moves=on_moves, on_ply=on_ply, every=self.exchange_every)
-        eng.check()
+        return on_moves, on_ply
 
     # ------------------------------------------------------------------ one process per GPU
     def _ranks(self, gpus):
@@ -314,6 +323,7 @@ class SelfPlayScheduler:
             self._play_games(self.epoch_length, update=True)
             saved = os.path.join(self.save_dir, self.start_time,
                                  "model-" + datetime.datetime.now().isoformat() + ":" + str(self.epoch_length * (epoch + 1)))
+            self.trainer.sync()  # the weights after every queued SGD step
             if self.rank == 0:
                 torch.save({"model": self.network.state_dict()}, saved)
             D.broadcast_state_dict(self.network)
@@ -345,22 +355,20 @@ class SelfPlayScheduler:
         gen = getattr(c, "policy_gen", None)
         name = getattr(gen, "__name__", "").lower()
         if name in ("random", "onesteplookahead"):
-            return ("random" if name == "random" else "lookahead"), None
+            return ("random" if name == "random" else "lookahead"), {}
         kw = dict(getattr(c, "policy_kwargs", {}) or {})
         net = self.evaluation_network
         if net is None:
             net = kw.get("network", kw.get("evaluator"))
         if net is None:
             raise ValueError("the evaluation MCTreeSearch has no network (pass evaluation_network=)")
-        pk = self._policy_kwargs()
-        for key, default in (("alpha", 1), ("strong_play", False)):
-            if kw.get(key, default) != pk.get(key, default):
-                logging.warning(f"evaluation policy {key}={kw.get(key, default)} differs from the policy's; "
-                                f"the arena uses the policy's value for both sides")
-        return net, kw.get("iterations", 100)
+        # the opponent's own MCTreeSearch kwargs (mcts.py:119-136 defaults), per side in the arena
+        return net, dict(opponent_iterations=kw.get("iterations", 100), opponent_alpha=kw.get("alpha", 1),
+                         opponent_strong_play=kw.get("strong_play", False),
+                         opponent_search_threads=self._opponent_threads)
 
     def _evaluation_engine(self, n_games):
-        opponent, opp_iters = self._opponent()
+        opponent, opp_kw = self._opponent()
         kw = self._policy_kwargs()
         per_rank = max(1, n_games // self.world + (1 if self.rank < n_games % self.world else 0))
         slots = min(per_rank, self.n_games or 4096)
@@ -368,8 +376,7 @@ class SelfPlayScheduler:
         return SelfPlayEngine(self.game, self.network, n_games=slots, iterations=kw.get("iterations", 100),
                               alpha=kw.get("alpha", 1), strong_play=kw.get("strong_play", False), evaluate=True,
                               seed=self.seed + 104729 + 7919 * self.rank, device=self.device, opponent=opponent,
-                              opponent_iterations=opp_iters, record=False,
-                              search_threads=self._search_threads), per_rank
+                              record=False, search_threads=self._search_threads, **opp_kw), per_rank
 
     def _play_evaluation(self, n_games):
         """n_games evaluation games over all ranks (task i -> swap_sides = i odd, update=False);
@@ -466,12 +473,23 @@ def _scheduler_rank(kwargs, method, call_kwargs, result_q):
 
 class _Trainer:
     """UpdateWorker core (updateworker.py:119-149) on the same device: AZ-loss SGD steps on batches
-    sampled from the device replay ring (replay.DeviceReplay), LR on plateau."""
+    sampled from the device replay ring (replay.DeviceReplay), LR on plateau.
+
+    The reference's UpdateWorker trains in its own process while the workers play
+    (updateworker.py:141-149).  Here `step()` enqueues the update on a HIP stream of its own and
+    returns without a host synchronisation, so the SGD kernels run beside the arena's next ply
+    (self-play evaluates leaves with its own packed copy of the epoch-start weights, refreshed at
+    epoch boundaries).  `sync()` makes the current stream wait for the queued steps: before replay
+    rows are overwritten and before the weights are read (checkpoint, weight refresh)."""
 
     def __init__(self, network, optim, memory_size, batch_size, min_memory, q_average, device, W=7, H=6, A=7,
-                 train_mode=True):
+                 train_mode=True, overlap=True):
         from .replay import DeviceReplay
 
+        dev = torch.device(device) if device is not None else torch.device("cpu")
+        self.stream = torch.cuda.Stream(device=dev) if overlap and dev.type == "cuda" else None
+        self.steps = 0
+        self.last_loss = None  # device tensor of the latest queued step
         self.network = network
         self.optim = optim
         self.memory = DeviceReplay(memory_size, W, H, A, device=device)
@@ -488,21 +506,37 @@ class _Trainer:
             self.memory.add(queue.get())
 
     def step(self):
-        """One update (mcts.py:254-270): uniform batch without replacement from the device ring."""
+        """One update (mcts.py:254-270): uniform batch without replacement from the device ring.
+        With a trainer stream: queued there (after the rows added so far), no host sync; returns
+        the loss as a device tensor."""
         if len(self.memory) < max(self.batch_size, self.min_memory):
             return None
-        return self.train_batch(*self.memory.sample_batch(self.batch_size))
+        self.steps += 1
+        if self.stream is None:
+            return self.train_batch(*self.memory.sample_batch(self.batch_size))
+        self.stream.wait_stream(torch.cuda.current_stream(self.stream.device))
+        with torch.cuda.stream(self.stream):
+            self.last_loss = self._train_step(*self.memory.sample_batch(self.batch_size))
+        return self.last_loss
 
-    def train_batch(self, s, z, pi, q):
-        """loss (mcts.py:234-252, via mcts.az_loss) -> zero_grad -> backward -> SGD step, with the
-        network in train mode as the UpdateWorker runs it (updateworker.py:63); pinned by G8."""
+    def sync(self):
+        """The current stream waits for the queued training steps (GPU-side, no host sync)."""
+        if self.stream is not None:
+            torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)
+
+    def _train_step(self, s, z, pi, q):
         self.network.train(self.train_mode)
         loss = az_loss(self.network, s, z, pi, q, self.q_average)
         self.optim.zero_grad()
         loss.backward()
         self.optim.step()
         self.network.eval()
-        return float(loss.detach())
+        return loss.detach()
+
+    def train_batch(self, s, z, pi, q):
+        """loss (mcts.py:234-252, via mcts.az_loss) -> zero_grad -> backward -> SGD step, with the
+        network in train mode as the UpdateWorker runs it (updateworker.py:63); pinned by G8."""
+        return float(self._train_step(s, z, pi, q))
 
     def lr_step(self, reward):
         self.scheduler.step(reward)

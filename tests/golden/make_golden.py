@@ -28,7 +28,9 @@ Fixtures
      against a second MCTreeSearch with its own table net and its own iteration
      count, or against the hard-coded OneStepLookahead / Random players
      (games/general/hardcoded_players.py), whose `random.choice` draws are logged
-     as (n, index).
+     as (n, index).  Later rows give the two MCTreeSearch sides their own
+     alpha / strong_play (each side is built from its own container's kwargs,
+     selfplayworker.py:71-81, mcts.py:119-136).
 
     python tests/golden/make_golden.py G5     # regenerate one fixture only
 """
@@ -97,18 +99,23 @@ def gen_arena_games(ref_mcts, SelfPlayer, Connect4Env, TicTacToeEnv):
 
     MCTreeSearch._play = spy_play
     hp.random = _ChoiceSpy(choices)
-    plan = [  # game, EnvCls, A, policy sims, opponent kind, opponent sims, count
+    plan = [  # game, EnvCls, A, policy sims, opponent kind, opponent sims, count[, policy kw, opponent kw]
         ("connect4", Connect4Env, 7, 25, "mcts", 40, 8),
         ("tictactoe", TicTacToeEnv, 9, 25, "mcts", 10, 8),
         ("connect4", Connect4Env, 7, 25, "lookahead", 0, 8),
         ("connect4", Connect4Env, 7, 25, "random", 0, 6),
         ("tictactoe", TicTacToeEnv, 9, 25, "lookahead", 0, 8),
         ("tictactoe", TicTacToeEnv, 9, 25, "random", 0, 6),
+        # per-side search settings (round 3): the two sides differ in alpha and strong_play
+        ("connect4", Connect4Env, 7, 25, "mcts", 30, 8, dict(alpha=1), dict(alpha=0.3, strong_play=True)),
+        ("tictactoe", TicTacToeEnv, 9, 25, "mcts", 15, 8, dict(alpha=0.15, strong_play=True), dict(alpha=1)),
+        ("connect4", Connect4Env, 7, 20, "mcts", 20, 6, dict(strong_play=True), dict(alpha=2.0)),
     ]
     games = []
     gid = 0
     try:
-        for game, EnvCls, A, sims, kind, opp_sims, count in plan:
+        for game, EnvCls, A, sims, kind, opp_sims, count, *kws in plan:
+            pkw, okw = (kws + [{}, {}])[:2]
             for k in range(count):
                 seed = 50_000 + gid
                 swap = bool(k % 2)
@@ -116,11 +123,12 @@ def gen_arena_games(ref_mcts, SelfPlayer, Connect4Env, TicTacToeEnv):
                 np.random.seed(seed)
                 random.seed(seed)
                 rq = _ListQueue()
-                pol = MCTreeSearch(network=TableNet(A, salt=salt_p), env=EnvCls, memory_queue=None, iterations=sims)
+                pol = MCTreeSearch(network=TableNet(A, salt=salt_p), env=EnvCls, memory_queue=None, iterations=sims,
+                                   **pkw)
                 pol.train(False)
                 if kind == "mcts":
                     opp = MCTreeSearch(network=TableNet(A, salt=salt_o), env=EnvCls, memory_queue=None,
-                                       iterations=opp_sims)
+                                       iterations=opp_sims, **okw)
                     opp._golden_tree = 1
                 elif kind == "lookahead":
                     opp = hp.OneStepLookahead(env=EnvCls)
@@ -137,6 +145,7 @@ def gen_arena_games(ref_mcts, SelfPlayer, Connect4Env, TicTacToeEnv):
                 states, r = sp.play_episode(swap_sides=swap, update=False)
                 games.append(dict(
                     id=gid, game=game, sims=sims, opponent=kind, opponent_sims=opp_sims, seed=seed,
+                    policy_kwargs=pkw, opponent_kwargs=okw,
                     swap_sides=swap, salt_policy=salt_p, salt_opponent=salt_o, result=int(r),
                     results_queue=[dict(reward=int(x["reward"]), swap_sides=bool(x["swap_sides"])) for x in rq.items],
                     plies=[dict(x) for x in log], choices=[list(c) for c in choices],

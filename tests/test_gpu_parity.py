@@ -183,11 +183,15 @@ def _check_g3(games, moves, counters):
 
 
 def _g5_groups():
+    import json
+
     games = load_json("arena_games.json")
-    return sorted(group_by(games, ["game", "sims", "opponent", "opponent_sims"]).items())
+    for g in games:  # per-side kwargs are part of a group's identity (one arena per group)
+        g["_kw"] = json.dumps([g.get("policy_kwargs") or {}, g.get("opponent_kwargs") or {}], sort_keys=True)
+    return sorted(group_by(games, ["game", "sims", "opponent", "opponent_sims", "_kw"]).items())
 
 
-@pytest.mark.parametrize("key", [k for k, _ in _g5_groups()], ids=lambda k: f"{k[0]}-{k[2]}-{k[1]}v{k[3]}")
+@pytest.mark.parametrize("key", [k for k, _ in _g5_groups()], ids=lambda k: f"{k[0]}-{k[2]}-{k[1]}v{k[3]}" + ("-kw" if k[4] != "[{}, {}]" else ""))
 def test_evaluation_games_match_reference(key):
     """G5 on the two-player arena: a second network in its own row segment with its own
     iteration budget, or the hard-coded OneStepLookahead / Random players on device."""
@@ -312,7 +316,7 @@ def test_threaded_selfplay_games_match_oracle(key, threads, recycle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("key", [k for k, _ in _g5_groups()], ids=lambda k: f"{k[0]}-{k[2]}-{k[1]}v{k[3]}")
+@pytest.mark.parametrize("key", [k for k, _ in _g5_groups()], ids=lambda k: f"{k[0]}-{k[2]}-{k[1]}v{k[3]}" + ("-kw" if k[4] != "[{}, {}]" else ""))
 def test_threaded_evaluation_games_match_oracle(key):
     """G5 evaluation games with 4 sims in flight per MCTS tree: two networks in row segments of
     n_trees * K rows each side of seg1 = n0 * K, per-player budgets cutting the last step;
@@ -326,6 +330,34 @@ def test_threaded_evaluation_games_match_oracle(key):
     exp = np.zeros((2, 3), dtype=np.int64)
     for g, (r, _, _, _) in zip(games, oracle):
         exp[int(g["swap_sides"])][{1: 0, 0: 1, -1: 2}[r]] += 1
+    assert np.array_equal(np.array(counters["results"]), exp)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k0,k1", [(4, 1), (2, 4)])
+@pytest.mark.parametrize("key", [k for k, _ in _g5_groups() if k[2] == "mcts"],
+                         ids=lambda k: f"{k[0]}-{k[1]}v{k[3]}" + ("-kw" if k[4] != "[{}, {}]" else ""))
+def test_evaluation_games_per_side_threads_match_oracle(key, k0, k1):
+    """Each side searches with its own thread_count (sims in flight per tree, spmcts_set_tree_search):
+    the policy with k0, the opponent MCTreeSearch with k1 (1 = the sequential search), on top of their
+    own alpha / strong_play / iterations; every Move and result bit-exact vs the oracle's episodes."""
+    from tests.parity_helpers import run_g5_group
+
+    games = dict(_g5_groups())[key]
+    moves, counters, oracle, _ = run_g5_group(games, search_threads=k0, opponent_threads=k1)
+    assert counters["error_flags"] == 0 and counters["games_finished"] == len(games)
+    by_game = {}
+    for i in range(len(moves["z"])):
+        by_game.setdefault(int(moves["game"][i]), []).append(i)
+    exp = np.zeros((2, 3), dtype=np.int64)
+    for gi, (g, (r, omoves, _, _)) in enumerate(zip(games, oracle)):
+        exp[int(g["swap_sides"])][{1: 0, 0: 1, -1: 2}[r]] += 1
+        got = by_game.get(gi, [])
+        assert len(got) == len(omoves), gi
+        for i, M in zip(got, omoves):
+            assert moves["tree_probs"][i].astype(float).tolist() == M["tree_probs"].astype(float).tolist(), (gi, i)
+            q = np.float64(moves["q"][i]) if moves["q_f64"][i] else np.float32(moves["q"][i])
+            assert float(q) == float(M["q"]), (gi, i)
     assert np.array_equal(np.array(counters["results"]), exp)
     by_game = {}
     for i in range(len(moves["z"])):

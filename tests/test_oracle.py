@@ -129,14 +129,18 @@ def _g5_run(g, rng_p=None, rng_o=None):
     rng = NumpyRNG()
     if g["opponent"] != "mcts":
         rng_o = rng_o or PyRandomRNG(g["seed"])  # random.seed(seed) in the generator
+    pkw, okw = g.get("policy_kwargs") or {}, g.get("opponent_kwargs") or {}
     return play_episode(g["game"], net_p, net_o, rng_p or rng, rng_o or rng, g["sims"],
                         swap_sides=g["swap_sides"], update=False, evaluate=True, opponent=g["opponent"],
-                        opponent_iterations=g["opponent_sims"] or None)
+                        opponent_iterations=g["opponent_sims"] or None, alpha=pkw.get("alpha", 1),
+                        strong_play=pkw.get("strong_play", False), opponent_alpha=okw.get("alpha", 1),
+                        opponent_strong_play=okw.get("strong_play", False))
 
 
-@pytest.mark.parametrize("idx", range(44))
+@pytest.mark.parametrize("idx", range(66))
 def test_evaluation_games_match_reference(idx):
-    """G5: policy vs a second network with its own iteration count, or vs OneStepLookahead / Random."""
+    """G5: policy vs a second network with its own iteration count (and, games 44-65, its own alpha /
+    strong_play), or vs OneStepLookahead / Random."""
     g = load_json("arena_games.json")[idx]
     r, moves, log, (pol, opp, env) = _g5_run(g)
     assert r == g["result"] and moves == []
