@@ -24,6 +24,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <utility>
+
 #include "spmcts.h"
 #include "tower_edge.h"
 
@@ -1019,6 +1021,8 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
   head_layer<K>(X, w, b, out, board0, batch, wave, lane);
 }
 
+#include "tower_ring.h"
+
 template <class K>
 __global__ __launch_bounds__(K::THREADS) __attribute__((amdgpu_waves_per_eu(K::WAVES / 4 * K::OCC, K::WAVES / 4 * K::OCC))) void k_tower(
     const __bf16 *planes, int batch, int n_blocks, const bf16x8 *wpk, const float *bias, uint16_t *out) {
@@ -1452,6 +1456,40 @@ static int forward_dev(int32_t width, int32_t height, int32_t channels, int32_t 
 }
 }  // namespace tower
 
+namespace tower {
+// Ring trunk launch (tower_ring.h): full 6-board tiles only, for the C = 128 Connect4 net with at most
+// ring::MAX_CONVS / 2 blocks.  count == nullptr: the batch is max_batch.
+template <class E>
+static int launch_ring(const void *planes, const int32_t *count, int max_batch, int n_blocks, const void *w,
+                       const float *b, void *out, hipStream_t s) {
+  using K = Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true, true, E>;
+  if (2 * n_blocks > ring::MAX_CONVS) return -2;
+  const int grid = (max_batch + K::BOARDS - 1) / K::BOARDS;
+  if (grid <= 0) return 0;
+  const int lds = ring::Geo<K>::lds(2 * n_blocks);
+  static int attr = 0;
+  if (lds > attr) {
+    if (hipFuncSetAttribute((const void *)ring::k_tower_ring<K>, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
+        hipSuccess)
+      return -10;
+    attr = lds;
+  }
+  hipLaunchKernelGGL(ring::k_tower_ring<K>, dim3(grid), dim3(256), lds, s, (const __bf16 *)planes, count, max_batch,
+                     n_blocks, (const bf16x8 *)w, b, (uint16_t *)out);
+  return hipGetLastError() == hipSuccess ? 0 : -11;
+}
+
+// SPMCTS_TOWER_RING=0 keeps the two-buffer trunk for the C = 128 Connect4 net (A/B switch, read once)
+static bool ring_enabled(int n_blocks) {
+  static int on = -1;
+  if (on < 0) {
+    const char *e = getenv("SPMCTS_TOWER_RING");
+    on = e ? atoi(e) != 0 : 1;
+  }
+  return on && 2 * n_blocks <= ring::MAX_CONVS;
+}
+}  // namespace tower
+
 extern "C" int spmcts_tower_forward_dev(int32_t width, int32_t height, int32_t channels, int32_t n_blocks,
                                         const void *planes_dev, const int32_t *count_dev, int32_t max_batch,
                                         const void *weights_dev, const float *bias_dev, void *features_dev,
@@ -1461,6 +1499,9 @@ extern "C" int spmcts_tower_forward_dev(int32_t width, int32_t height, int32_t c
   if (n_blocks < 0 || max_batch < 0 || !count_dev || (flags & ~(SPMCTS_TOWER_PACK | SPMCTS_TOWER_F16))) return -3;
   if (max_batch == 0) return 0;
   const bool pack = (flags & SPMCTS_TOWER_PACK) != 0;
+  if (width == 7 && height == 6 && channels == 128 && ring_enabled(n_blocks))
+    return (flags & SPMCTS_TOWER_F16 ? launch_ring<_Float16> : launch_ring<__bf16>)(
+        planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, s);
   if (flags & SPMCTS_TOWER_F16)
     return forward_dev<_Float16>(width, height, channels, n_blocks, planes_dev, count_dev, max_batch, weights_dev,
                                  bias_dev, features_dev, pack, s);
@@ -1474,6 +1515,9 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
   using namespace tower;
   hipStream_t s = (hipStream_t)stream;
   if (n_blocks < 0 || batch < 0 || (flags & ~SPMCTS_TOWER_F16)) return -3;
+  if (width == 7 && height == 6 && channels == 128 && ring_enabled(n_blocks) && !getenv("SPMCTS_TOWER_CG"))
+    return (flags & SPMCTS_TOWER_F16 ? launch_ring<_Float16> : launch_ring<__bf16>)(
+        planes_dev, nullptr, batch, n_blocks, weights_dev, bias_dev, features_dev, s);
   if (flags & SPMCTS_TOWER_F16) {  // the shipped tile set only (the SPMCTS_TOWER_CG variants are bf16 timing studies)
     const char *pl = (const char *)planes_dev;
     char *ft = (char *)features_dev;

@@ -228,7 +228,8 @@ def test_evaluation_games_without_records():
     """update=False: no Move records, same results."""
     from tests.parity_helpers import run_g5_group
 
-    games = [g for g in load_json("arena_games.json") if g["opponent"] == "mcts" and g["game"] == "connect4"]
+    games = [g for g in load_json("arena_games.json") if g["opponent"] == "mcts" and g["game"] == "connect4"
+             and g["opponent_sims"] == 40 and not g.get("policy_kwargs") and not g.get("opponent_kwargs")]
     moves, counters, _, _ = run_g5_group(games, record=False)
     assert moves is None and counters["positions_exported"] == 0
     assert counters["games_finished"] == len(games)
