@@ -1479,12 +1479,13 @@ static int launch_ring(const void *planes, const int32_t *count, int max_batch, 
   return hipGetLastError() == hipSuccess ? 0 : -11;
 }
 
-// SPMCTS_TOWER_RING=0 keeps the two-buffer trunk for the C = 128 Connect4 net (A/B switch, read once)
+// SPMCTS_TOWER_RING=1 runs the ring trunk for the C = 128 Connect4 net instead of the two-buffer trunk
+// (an A/B switch, read once; measured 3-6 % slower, DESIGN.md §4 "Weight ring in LDS")
 static bool ring_enabled(int n_blocks) {
   static int on = -1;
   if (on < 0) {
     const char *e = getenv("SPMCTS_TOWER_RING");
-    on = e ? atoi(e) != 0 : 1;
+    on = e ? atoi(e) != 0 : 0;
   }
   return on && 2 * n_blocks <= ring::MAX_CONVS;
 }

@@ -27,6 +27,13 @@
 
 namespace ring {
 
+// timing ablations (wrong results; kernel analysis only): 1 = no DMAs in the k-loop, 2 = no phase
+// barriers, 4 = no A-fragment reads from the ring
+#ifndef SPMCTS_RING_ABL
+#define SPMCTS_RING_ABL 0
+#endif
+constexpr int ABL = SPMCTS_RING_ABL;
+
 constexpr int KK = 8;          // k-steps per tap (C = 128: 8 x 16 input channels)
 constexpr int STEPS = 9 * KK;  // k-steps per conv layer
 constexpr int R = 8;           // ring slots, one k-step (4 fragments) each
@@ -88,6 +95,13 @@ struct Geo {
       if (live(mg, t, kOrd.tap[i])) return i;
     return STEPS;
   }
+  // tiles whose accumulators start from zero at step i (a mask, so kernels test it at compile time)
+  static constexpr uint32_t zmask(int mg, int i) {
+    uint32_t m = 0;
+    for (int t = 0; t < K::NT; ++t)
+      if (first(mg, t) == i) m |= 1u << t;
+    return m;
+  }
   // phases (pairs of steps) are balanced: both row halves issue the same number of MFMAs
   static constexpr bool balanced() {
     for (int i = 0; i < STEPS; i += 2)
@@ -135,16 +149,22 @@ __device__ __forceinline__ void ring_step(char *smem, const Wave<K> &w, f32x16 (
   constexpr int KKN = HAS_NEXT ? kOrd.kk[I + 1] : 0;
   constexpr uint32_t LVN = HAS_NEXT ? G::lmask(MG_, TAPN) : 0u;
   constexpr int NDS = K::MT + G::popc(LVN);  // LDS reads issued this step (next step's A and B)
+  constexpr uint32_t ZM = G::zmask(MG_, I);  // tiles starting from zero here
   const int J = L * STEPS + I;
   char *ring = smem + G::RING;
   // DMA of step J + D (this wave's fragment); past the last layer the last layer is re-read (keeps the
   // per-phase DMA count; the slot it lands in has been consumed)
-  if constexpr (I + D < STEPS)
+  if constexpr (ABL & 1) {
+  } else if constexpr (I + D < STEPS) {
     issue_dma<I + D>(ring, wconv, L, (J + D) % R, ct, w.lane);
-  else
+  } else {
     issue_dma<I + D - STEPS>(ring, wconv, L + 1 < n_convs ? L + 1 : L, (J + D) % R, ct, w.lane);
+  }
   // A fragments of the next step (the next layer's step 0 after the last step)
-  {
+  if constexpr (ABL & 4) {
+#pragma unroll
+    for (int m = 0; m < K::MT; ++m) anext[m] = acur[m];
+  } else {
     const char *slot = ring + ((J + 1) % R) * SLOT + w.lane * 16;
 #pragma unroll
     for (int m = 0; m < K::MT; ++m) anext[m] = *(const bf16x8 *)(slot + (w.cg * K::MT + m) * FRAG);
@@ -160,7 +180,7 @@ __device__ __forceinline__ void ring_step(char *smem, const Wave<K> &w, f32x16 (
 #pragma unroll
     for (int m = 0; m < K::MT; ++m)
       if ((LV >> t) & 1u) {
-        if (G::first(MG_, t) == I)
+        if ((ZM >> t) & 1u)
           acc[m][t] = K::mfma(acur[m], bcur[t], f32x16{});
         else
           acc[m][t] = K::mfma(acur[m], bcur[t], acc[m][t]);
@@ -185,7 +205,7 @@ __device__ __forceinline__ void ring_step(char *smem, const Wave<K> &w, f32x16 (
     // and every wave's DMA may overwrite the slots read before it
     asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-    __builtin_amdgcn_s_barrier();
+    if constexpr (!(ABL & 2)) __builtin_amdgcn_s_barrier();
   }
 }
 

@@ -185,3 +185,48 @@ def test_fp16_bench_nets_finite_and_close(ff):
     e_hip = max((p - ref_p).abs().max().item(), (v - ref_v.view(-1)).abs().max().item())
     e_ac = max((ap.float() - ref_p).abs().max().item(), (av.float() - ref_v).abs().max().item())
     assert e_hip <= 2 * e_ac + 2e-3, (e_hip, e_ac)
+
+
+_RING_CHILD = r"""
+import json, sys, torch
+sys.path.insert(0, {repo!r})
+from self_play_reinforcement_learning_amd.evaluator import HipTowerEvaluator
+from tests.test_gpu_tower import _net, _planes
+out = {{}}
+for dt in (torch.bfloat16, torch.float16):
+    net = _net(7, 6, 7, 20, 32)
+    x = _planes(7, 6, 999)
+    with torch.no_grad():
+        rp, rv = net.forward_planes(x)
+    hip = HipTowerEvaluator(net, dtype=dt)
+    xb = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    p, v = hip(xb)
+    cnt = torch.tensor([999], dtype=torch.int32, device=x.device)
+    pd, vd = hip.forward_dev(xb, cnt, 999)
+    torch.cuda.synchronize()
+    p7, v7 = hip(xb[:7].contiguous(memory_format=torch.channels_last))
+    out[str(dt)] = dict(err=max((p - rp).abs().max().item(), (v - rv.view(-1)).abs().max().item()),
+                        dev_equal=bool(torch.equal(pd[:999], p) and torch.equal(vd[:999].view(-1), v.view(-1))),
+                        batch_equal=bool(torch.equal(p7, p[:7]) and torch.equal(v7, v[:7])))
+print(json.dumps(out))
+"""
+
+
+def test_ring_trunk_variant():
+    """The LDS weight-ring trunk (csrc/tower_ring.h, SPMCTS_TOWER_RING=1: read once per process, so it
+    runs in a child process): the same tolerance against the fp32 forward as the default trunk
+    (test_tower_matches_fp32_reference's 0.05 bound), bit-identical device-count and host-count
+    outputs, and batch independence.  Measured slower than the default trunk."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SPMCTS_TOWER_RING="1")
+    r = subprocess.run([sys.executable, "-c", _RING_CHILD.format(repo=repo)], env=env, capture_output=True, text=True,
+                       timeout=240, cwd=repo)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    for dt, d in res.items():
+        assert d["err"] < 0.05 and d["dev_equal"] and d["batch_equal"], (dt, d)
