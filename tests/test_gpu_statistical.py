@@ -302,12 +302,14 @@ def test_fused_tower_search_shift(pi, precision):
     assert (np.abs(fc - fg) <= 4.5 * sef + tol).all(), (fc.round(4), fg.round(4))
 
 
-@pytest.mark.parametrize("variant", ["sims100", "alpha0.3"])
+@pytest.mark.parametrize("variant", ["sims100", "serial"])
 def test_resnet_statistical_check_has_power(variant):
     """Negative control at the headline net: the fp16-tower comparison at its stated bound (4.5 SE + 0.01)
     rejects, against the reference's threaded ResNet samples, a search with half the simulation budget
-    (100 instead of 200) and one whose root noise is drawn with Dirichlet alpha 0.3 instead of the
-    reference's 1 (mcts.py:135)."""
+    (100 instead of 200) and one run serially (1 simulation in flight instead of the reference's
+    thread_count with virtual loss, mcts.py:229-262).  Root noise drawn with Dirichlet alpha 0.3 instead
+    of 1 (mcts.py:135) moved the mean visit fractions of this position by at most 0.004 (measured round 3),
+    inside the 0.01 bound: a difference of that size is below what this check resolves."""
     d = _g6("resnet_single")
     pos = d["positions"][2]
     cp, _ = _ref_samples(pos)
@@ -315,7 +317,7 @@ def test_resnet_statistical_check_has_power(variant):
     if variant == "sims100":
         gp, _, _ = _gpu_threaded(pos["opening"], 4096, 100, d["thread_count"], net=ev)
     else:
-        gp, _, _ = _gpu_threaded(pos["opening"], 4096, d["sims"], d["thread_count"], net=ev, alpha=0.3)
+        gp, _, _ = _gpu_threaded(pos["opening"], 4096, d["sims"], 1, net=ev)
     se = np.sqrt(cp.var(0, ddof=1) / len(cp) + gp.var(0, ddof=1) / len(gp))
     assert not (np.abs(gp.mean(0) - cp.mean(0)) <= 4.5 * se + SHIFT_TOL["fp16"]).all(), \
         (gp.mean(0).round(4), cp.mean(0).round(4), se.round(4))
