@@ -224,6 +224,8 @@ def main():
                     help="node blocks per tree; below the worst case the arena recycles subtrees (k_compact)")
     ap.add_argument("--no-pack", action="store_true",
                     help="lanes > 1: keep round-aligned tower tiles (no SPMCTS_TOWER_PACK)")
+    ap.add_argument("--progress", action="store_true",
+                    help="one stderr line per untimed ply (long warm-ups, e.g. config 3 in steady state)")
     ap.add_argument("--dtype", choices=["bf16", "fp16"], default="bf16",
                     help="element type of the fused trunk's weights / activations (fp32 accumulation); fp16 is the "
                          "reference's own inference dtype (amp.autocast, inference_worker.py:117)")
@@ -291,8 +293,12 @@ def main():
         eng.ply(on_moves=ex.stage if not (args.no_gather or arena_mode) else None)
         ex.end_ply(eng.stats_vector)
 
-    for _ in range(args.warmup):
+    tw = time.perf_counter()
+    for i in range(args.warmup):
         one_step()
+        if args.progress and rank == 0:
+            print(f"bench.py: warm-up ply {i + 1}/{args.warmup} at {time.perf_counter() - tw:.1f} s", file=sys.stderr,
+                  flush=True)
     if D.is_distributed() and args.warmup % args.exchange_every:
         ex.end_ply(eng.stats_vector, force=True)
     ex._plies = ex.rounds = ex.rows_gathered = 0  # the timed region starts a fresh episode batch

@@ -4,10 +4,10 @@
 // MCTreeSearch) and the episode loop of games/algos/selfplayworker.py
 // (SelfPlayer) with one device-resident arena:
 //
-//   node store   SoA, one "child block" per expansion: n[APAD] i32, w[APAD] f64,
-//                p[APAD] f32, child[APAD] i32 (local block of the child's own
-//                children, -1 = unexpanded), vmask u32 per block (valid children).
-//                A node = (block, slot); trees own disjoint block ranges.
+//   node store   one 32*APAD-byte record per "child block" (one per expansion):
+//                n, vl, child (local block of the child's own children, -1 =
+//                unexpanded), p, w, f64 flag per slot + the valid-children mask
+//                (NodeRec).  A node = (block, slot); trees own disjoint block ranges.
 //   trees        root node, root board (2 x u64 bitboards), root player, bump
 //                allocator, Dirichlet noise, per-sim path scratch, RNG.
 //   games        SelfPlayer state machine: board (policy frame), ply, swap_sides,
@@ -82,14 +82,8 @@ struct View {
   int K, NS;  // simulations in flight per tree (virtual loss; 1 = sequential), pending slots = T * K
   double cpuct, x, alpha;
   int strong, evaluate, rng_mode, leaf_format, leaf_layout;
-  // node store
-  int32_t *bn;
-  double *bw;
-  float *bp;
-  int32_t *bc;
-  uint32_t *bvm;
-  uint8_t *bf64;  // "w is a numpy float64" (strong_play dtype quirk, mcts.py:287/:308)
-  int32_t *bvl;   // MCNode.virtual_loss (mcts.py:44), allocated only when K > 1
+  // node store: one record of 32 * P bytes per child block (nd_* below)
+  char *nodes;
   // trees
   int32_t *root;
   uint64_t *rpos, *rneg;
@@ -163,6 +157,51 @@ struct View {
   int32_t record;    // games mode: keep Move records (play_episode update=True)
   int32_t sim;       // index of the current simulation within the search (by value per launch)
 };
+
+// Node store.  A child block (the A children of one expanded node, P = APAD slots) is ONE contiguous
+// record of 32 * P bytes: n i32[P] | vl i32[P] | child-block i32[P] | p f32[P] | w f64[P] | f64 flag
+// u8[P] | valid-children mask u32 | pad.  The fields a select level scores (n, vl, child, p: the first
+// 16 P bytes; w, the mask: the next) lie in two 128-byte lines for Connect4 (P = 8) instead of one line
+// per field array.  Node id i = (tree * cap + block) * P + slot, as before; the flag is "w is a numpy
+// float64" (strong_play dtype quirk, mcts.py:287/:308), vl is MCNode.virtual_loss (mcts.py:44).
+template <int P>
+struct NodeRec {
+  static constexpr int N = 0, VL = 4 * P, C = 8 * P, PR = 12 * P, W = 16 * P, F = 24 * P, VM = 25 * P, BYTES = 32 * P;
+  static_assert(VM + 4 <= BYTES && W % 8 == 0 && VM % 4 == 0, "record layout");
+};
+template <int P>
+__host__ __device__ __forceinline__ char *nd_rec(const View &v, size_t i) {
+  return v.nodes + (i / P) * (size_t)NodeRec<P>::BYTES;
+}
+template <int P>
+__host__ __device__ __forceinline__ int32_t &nd_n(const View &v, size_t i) {
+  return ((int32_t *)(nd_rec<P>(v, i) + NodeRec<P>::N))[i % P];
+}
+template <int P>
+__host__ __device__ __forceinline__ int32_t &nd_vl(const View &v, size_t i) {
+  return ((int32_t *)(nd_rec<P>(v, i) + NodeRec<P>::VL))[i % P];
+}
+template <int P>
+__host__ __device__ __forceinline__ int32_t &nd_c(const View &v, size_t i) {
+  return ((int32_t *)(nd_rec<P>(v, i) + NodeRec<P>::C))[i % P];
+}
+template <int P>
+__host__ __device__ __forceinline__ float &nd_p(const View &v, size_t i) {
+  return ((float *)(nd_rec<P>(v, i) + NodeRec<P>::PR))[i % P];
+}
+template <int P>
+__host__ __device__ __forceinline__ double &nd_w(const View &v, size_t i) {
+  return ((double *)(nd_rec<P>(v, i) + NodeRec<P>::W))[i % P];
+}
+template <int P>
+__host__ __device__ __forceinline__ uint8_t &nd_f(const View &v, size_t i) {
+  return ((uint8_t *)(nd_rec<P>(v, i) + NodeRec<P>::F))[i % P];
+}
+// valid-children mask of block `gb` = tree * cap + block
+template <int P>
+__host__ __device__ __forceinline__ uint32_t &nd_vm(const View &v, size_t gb) {
+  return *(uint32_t *)(v.nodes + gb * (size_t)NodeRec<P>::BYTES + NodeRec<P>::VM);
+}
 
 enum { C_SIMS = 0, C_NN = 1, C_TERM = 2, C_DEPTH = 3, C_SETNODE = 4, C_MOVES = 5, C_LEAK = 6, C_GC = 7, C_HWM = 8, C_NCNT = 10 };
 enum { GS_IDLE = 0, GS_ACTIVE = 1, GS_DONE = 2 };
@@ -271,24 +310,24 @@ __device__ __forceinline__ void reset_tree(const View &v, int tree, int player, 
   const size_t nb = nbase<G>(v, tree);
   const size_t bb = (size_t)tree * v.cap;
   // block 0 = pseudo block holding the root in slot 0; block 1 = root's children
-  v.bn[nb + 0] = 0;
-  v.bw[nb + 0] = 0.0;
-  v.bp[nb + 0] = 0.f;
-  v.bc[nb + 0] = 1;
-  v.bf64[nb + 0] = 0;
+  nd_n<P>(v, nb + 0) = 0;
+  nd_w<P>(v, nb + 0) = 0.0;
+  nd_p<P>(v, nb + 0) = 0.f;
+  nd_c<P>(v, nb + 0) = 1;
+  nd_f<P>(v, nb + 0) = 0;
   if (v.K > 1) {
-    v.bvl[nb + 0] = 0;
-    for (int j = 0; j < P; ++j) v.bvl[nb + P + j] = 0;
+    nd_vl<P>(v, nb + 0) = 0;
+    for (int j = 0; j < P; ++j) nd_vl<P>(v, nb + P + j) = 0;
   }
   for (int j = 0; j < P; ++j) {
-    v.bn[nb + P + j] = 0;
-    v.bw[nb + P + j] = 0.0;
-    v.bp[nb + P + j] = j < G::A ? prior[j] : 0.f;
-    v.bc[nb + P + j] = -1;
-    v.bf64[nb + P + j] = 0;
+    nd_n<P>(v, nb + P + j) = 0;
+    nd_w<P>(v, nb + P + j) = 0.0;
+    nd_p<P>(v, nb + P + j) = j < G::A ? prior[j] : 0.f;
+    nd_c<P>(v, nb + P + j) = -1;
+    nd_f<P>(v, nb + P + j) = 0;
   }
-  v.bvm[bb + 0] = 1u;
-  v.bvm[bb + 1] = legal_mask<G>(Board{0, 0});
+  nd_vm<P>(v, bb + 0) = 1u;
+  nd_vm<P>(v, bb + 1) = legal_mask<G>(Board{0, 0});
   v.used[tree] = 2;
   v.root[tree] = 0;
   v.rpos[tree] = 0;
@@ -398,7 +437,7 @@ __global__ __launch_bounds__(256) void k_compact(View v, int n_active) {
   int32_t *list = v.gc_list + bb;
   int32_t *map = v.gc_map + bb;
   const int root = v.root[tree];
-  const int croot = v.bc[nb + root];
+  const int croot = nd_c<P>(v, nb + root);
   // 1. live blocks: BFS from the root's child block
   if (tid == 0) {
     s_head = 0;
@@ -416,7 +455,7 @@ __global__ __launch_bounds__(256) void k_compact(View v, int n_active) {
     __syncthreads();
     for (int k = head * P + tid; k < tail * P; k += NT) {
       const int blk = list[k / P], j = k % P;
-      const int c = j < G::A ? v.bc[nb + (size_t)blk * P + j] : -1;
+      const int c = j < G::A ? nd_c<P>(v, nb + (size_t)blk * P + j) : -1;
       if (c >= 0) list[atomicAdd(&s_tail, 1)] = c;
     }
     __threadfence_block();
@@ -451,18 +490,18 @@ __global__ __launch_bounds__(256) void k_compact(View v, int n_active) {
   __syncthreads();
   // 3. the root record into block 0 slot 0 (block 0 is never a destination: live blocks map to >= 1)
   if (tid == 0) {
-    const int32_t rn = v.bn[nb + root];
-    const double rw = v.bw[nb + root];
-    const float rp = v.bp[nb + root];
-    const uint8_t rf = v.bf64[nb + root];
-    const int32_t rvl = v.K > 1 ? v.bvl[nb + root] : 0;
-    v.bn[nb] = rn;
-    v.bw[nb] = rw;
-    v.bp[nb] = rp;
-    v.bf64[nb] = rf;
-    v.bc[nb] = croot >= 0 ? map[croot] : croot;
-    if (v.K > 1) v.bvl[nb] = rvl;
-    v.bvm[bb] = 1u;
+    const int32_t rn = nd_n<P>(v, nb + root);
+    const double rw = nd_w<P>(v, nb + root);
+    const float rp = nd_p<P>(v, nb + root);
+    const uint8_t rf = nd_f<P>(v, nb + root);
+    const int32_t rvl = v.K > 1 ? nd_vl<P>(v, nb + root) : 0;
+    nd_n<P>(v, nb) = rn;
+    nd_w<P>(v, nb) = rw;
+    nd_p<P>(v, nb) = rp;
+    nd_f<P>(v, nb) = rf;
+    nd_c<P>(v, nb) = croot >= 0 ? map[croot] : croot;
+    if (v.K > 1) nd_vl<P>(v, nb) = rvl;
+    nd_vm<P>(v, bb) = 1u;
     v.root[tree] = 0;
   }
   __threadfence_block();
@@ -478,25 +517,25 @@ __global__ __launch_bounds__(256) void k_compact(View v, int n_active) {
     uint32_t vm = 0;
     if (dst >= 0) {
       const size_t i = nb + (size_t)b * P + j;
-      n = v.bn[i];
-      w = v.bw[i];
-      pr = v.bp[i];
-      c = v.bc[i];
-      f = v.bf64[i];
-      if (v.K > 1) vl = v.bvl[i];
-      if (j == 0) vm = v.bvm[bb + b];
+      n = nd_n<P>(v, i);
+      w = nd_w<P>(v, i);
+      pr = nd_p<P>(v, i);
+      c = nd_c<P>(v, i);
+      f = nd_f<P>(v, i);
+      if (v.K > 1) vl = nd_vl<P>(v, i);
+      if (j == 0) vm = nd_vm<P>(v, bb + b);
       if (c >= 0) c = map[c];
     }
     __syncthreads();
     if (dst >= 0) {
       const size_t o = nb + (size_t)dst * P + j;
-      v.bn[o] = n;
-      v.bw[o] = w;
-      v.bp[o] = pr;
-      v.bc[o] = c;
-      v.bf64[o] = f;
-      if (v.K > 1) v.bvl[o] = vl;
-      if (j == 0) v.bvm[bb + dst] = vm;
+      nd_n<P>(v, o) = n;
+      nd_w<P>(v, o) = w;
+      nd_p<P>(v, o) = pr;
+      nd_c<P>(v, o) = c;
+      nd_f<P>(v, o) = f;
+      if (v.K > 1) nd_vl<P>(v, o) = vl;
+      if (j == 0) nd_vm<P>(v, bb + dst) = vm;
     }
     __threadfence_block();
     __syncthreads();
@@ -558,11 +597,11 @@ __global__ __launch_bounds__(64) void k_select(View v, int n_active) {
   rng_load(v, tree, rng);
   bool terr = false;
 
-  int node_n = v.bn[nb + node];
-  double node_w = v.bw[nb + node];
+  int node_n = nd_n<P>(v, nb + node);
+  double node_w = nd_w<P>(v, nb + node);
   // the node's child block: read for the root; below it, the child entry read with the parent's
   // block already holds it (one dependent global load per level instead of two)
-  int cb = v.bc[nb + node];
+  int cb = nd_c<P>(v, nb + node);
   int depth = 0;
   for (;;) {
     if (lane == 0) {
@@ -574,16 +613,16 @@ __global__ __launch_bounds__(64) void k_select(View v, int n_active) {
       if (lane == 0) set_err(v, SPMCTS_ERR_STATE);
       return;
     }
-    const uint32_t vm = v.bvm[bb + cb];
+    const uint32_t vm = nd_vm<P>(v, bb + cb);
     const size_t ci = nb + (size_t)cb * P + lane;
     int cn = 0, cc = -1;
     double cw = 0.0;
     float cp = 0.f;
     if (lane < G::A) {
-      cn = v.bn[ci];
-      cw = v.bw[ci];
-      cp = v.bp[ci];
-      cc = v.bc[ci];
+      cn = nd_n<P>(v, ci);
+      cw = nd_w<P>(v, ci);
+      cp = nd_p<P>(v, ci);
+      cc = nd_c<P>(v, ci);
     }
     const int gbase = (threadIdx.x & 63) & ~(P - 1);
     // the jitter does not depend on the child block: drawn here, it overlaps the loads above
@@ -632,13 +671,13 @@ __global__ __launch_bounds__(64) void k_select(View v, int n_active) {
           const bool strong = v.tstrong[tree] != 0;
           for (int k = 0; k <= depth; ++k) {
             const size_t idx = nb + s_node[grp][k];
-            v.bn[idx] = s_n[grp][k] + 1;
-            v.bw[idx] = s_w[grp][k] + val;
-            if (strong) v.bf64[idx] = 1;
+            nd_n<P>(v, idx) = s_n[grp][k] + 1;
+            nd_w<P>(v, idx) = s_w[grp][k] + val;
+            if (strong) nd_f<P>(v, idx) = 1;
           }
-          v.bn[nb + child] = cn_a + 1;
-          v.bw[nb + child] = cw_a + val;
-          if (strong) v.bf64[nb + child] = 1;
+          nd_n<P>(v, nb + child) = cn_a + 1;
+          nd_w<P>(v, nb + child) = cw_a + val;
+          if (strong) nd_f<P>(v, nb + child) = 1;
           cnt[C_TERM] += 1;
         } else {
           // pending network evaluation: stash the path for k_expand
@@ -706,14 +745,15 @@ struct TreeRoot {
 
 template <class G>
 __device__ __forceinline__ TreeRoot load_root(const View &v, int tree) {
+  constexpr int P = G::APAD;
   const size_t nb = nbase<G>(v, tree);
   TreeRoot R;
   R.node = v.root[tree];
   R.b = Board{v.rpos[tree], v.rneg[tree]};
   R.player = v.rplayer[tree];
-  R.n = v.bn[nb + R.node];
-  R.vl = v.bvl[nb + R.node];
-  R.cb = v.bc[nb + R.node];
+  R.n = nd_n<P>(v, nb + R.node);
+  R.vl = nd_vl<P>(v, nb + R.node);
+  R.cb = nd_c<P>(v, nb + R.node);
   return R;
 }
 
@@ -744,23 +784,23 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
   for (;;) {
     if (lane == 0) {
       s_node[depth] = node;
-      v.bvl[nb + node] = node_vl;
+      nd_vl<P>(v, nb + node) = node_vl;
     }
     if (cb < 0) {
       if (lane == 0) set_err(v, SPMCTS_ERR_STATE);
       return SIM_ERROR;
     }
-    const uint32_t vm = v.bvm[bb + cb];
+    const uint32_t vm = nd_vm<P>(v, bb + cb);
     const size_t ci = nb + (size_t)cb * P + lane;
     int cn = 0, cc = -1, cvl = 0;
     double cw = 0.0;
     float cp = 0.f;
     if (lane < G::A) {
-      cn = v.bn[ci];
-      cw = v.bw[ci];
-      cp = v.bp[ci];
-      cc = v.bc[ci];
-      cvl = v.bvl[ci];
+      cn = nd_n<P>(v, ci);
+      cw = nd_w<P>(v, ci);
+      cp = nd_p<P>(v, ci);
+      cc = nd_c<P>(v, ci);
+      cvl = nd_vl<P>(v, ci);
     }
     // the jitter does not depend on the child block: drawn here, it overlaps the loads above
     bool terr_j = false;
@@ -803,15 +843,15 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
         const bool strong = v.tstrong[tree] != 0;
         for (int k = lane; k <= depth; k += P) {
           const size_t idx = nb + s_node[k];
-          v.bn[idx] += 1;
-          v.bw[idx] += val;
-          if (strong) v.bf64[idx] = 1;
-          v.bvl[idx] -= 1;
+          nd_n<P>(v, idx) += 1;
+          nd_w<P>(v, idx) += val;
+          if (strong) nd_f<P>(v, idx) = 1;
+          nd_vl<P>(v, idx) -= 1;
         }
         if (lane == 0) {
-          v.bn[nb + child] += 1;
-          v.bw[nb + child] += val;
-          if (strong) v.bf64[nb + child] = 1;
+          nd_n<P>(v, nb + child) += 1;
+          nd_w<P>(v, nb + child) += val;
+          if (strong) nd_f<P>(v, nb + child) = 1;
         }
         R.n += 1;  // the root is s_node[0]
         R.vl -= 1;
@@ -827,7 +867,7 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
           cnt[C_TERM] += 1;
         } else {
           // lock the leaf (mcts.py:359); the path was stashed above for the backup
-          v.bc[nb + child] = -2;
+          nd_c<P>(v, nb + child) = -2;
           v.plen[ps] = depth + 1;
           v.leaf[ps] = child;
           v.lpos[ps] = nb2.pos;
@@ -1105,11 +1145,11 @@ __global__ __launch_bounds__(64) void k_expand(View v, const float *probs0, cons
   // create_children (mcts.py:103-107): A children in action order, validity = valid_moves
   {
     const size_t ci = nb + (size_t)blk * P + lane;
-    v.bn[ci] = 0;
-    v.bw[ci] = 0.0;
-    v.bp[ci] = lane < G::A ? prow[lane] : 0.f;
-    v.bc[ci] = -1;
-    v.bf64[ci] = 0;
+    nd_n<P>(v, ci) = 0;
+    nd_w<P>(v, ci) = 0.0;
+    nd_p<P>(v, ci) = lane < G::A ? prow[lane] : 0.f;
+    nd_c<P>(v, ci) = -1;
+    nd_f<P>(v, ci) = 0;
   }
   const int mover = v.lmover[tree];
   // network(s, parent.player) returns value * player (modules.py:109-112)
@@ -1118,14 +1158,14 @@ __global__ __launch_bounds__(64) void k_expand(View v, const float *probs0, cons
   const size_t pb = (size_t)tree * G::MAXD;
   for (int k = lane; k < plen; k += P) {
     const size_t idx = nb + v.pnode[pb + k];
-    v.bn[idx] = v.pn[pb + k] + 1;
-    v.bw[idx] = v.pw[pb + k] + val;
+    nd_n<P>(v, idx) = v.pn[pb + k] + 1;
+    nd_w<P>(v, idx) = v.pw[pb + k] + val;
   }
   if (lane == 0) {
-    v.bvm[bb + blk] = legal_mask<G>(Board{v.lpos[tree], v.lneg[tree]});
-    v.bc[nb + leaf] = blk;
-    v.bn[nb + leaf] = v.leaf_n[tree] + 1;
-    v.bw[nb + leaf] = v.leaf_w[tree] + val;
+    nd_vm<P>(v, bb + blk) = legal_mask<G>(Board{v.lpos[tree], v.lneg[tree]});
+    nd_c<P>(v, nb + leaf) = blk;
+    nd_n<P>(v, nb + leaf) = v.leaf_n[tree] + 1;
+    nd_w<P>(v, nb + leaf) = v.leaf_w[tree] + val;
     v.used[tree] = blk + 1;
     v.need[tree] = 0;
     v.cnt[(size_t)tree * C_NCNT + C_NN] += 1;
@@ -1247,26 +1287,26 @@ __device__ __forceinline__ void expand_vl_body(View v, const float *probs0, cons
       ++used;
       {
         const size_t ci = nb + (size_t)blk * P + lane;
-        v.bn[ci] = 0;
-        v.bw[ci] = 0.0;
-        v.bp[ci] = lane < G::A ? s_pr[grp][j][lane] : 0.f;
-        v.bc[ci] = -1;
-        v.bf64[ci] = 0;
-        v.bvl[ci] = 0;
+        nd_n<P>(v, ci) = 0;
+        nd_w<P>(v, ci) = 0.0;
+        nd_p<P>(v, ci) = lane < G::A ? s_pr[grp][j][lane] : 0.f;
+        nd_c<P>(v, ci) = -1;
+        nd_f<P>(v, ci) = 0;
+        nd_vl<P>(v, ci) = 0;
       }
       const double val = (double)s_vr[grp][j] * (double)mover;
       // backup of the path (distinct nodes): one lane per path node, the node ids prefetched
       for (int k = lane; k < plen; k += P) {
         const size_t idx = nb + (k < P ? s_pnode[grp][j][k] : v.pnode[(size_t)ps * G::MAXD + k]);
-        v.bn[idx] += 1;
-        v.bw[idx] += val;
-        v.bvl[idx] -= 1;
+        nd_n<P>(v, idx) += 1;
+        nd_w<P>(v, idx) += val;
+        nd_vl<P>(v, idx) -= 1;
       }
       if (lane == 0) {
-        v.bvm[bb + blk] = legal_mask<G>(Board{lpos, lneg});
-        v.bc[nb + leaf] = blk;
-        v.bn[nb + leaf] += 1;
-        v.bw[nb + leaf] += val;
+        nd_vm<P>(v, bb + blk) = legal_mask<G>(Board{lpos, lneg});
+        nd_c<P>(v, nb + leaf) = blk;
+        nd_n<P>(v, nb + leaf) += 1;
+        nd_w<P>(v, nb + leaf) += val;
         v.used[tree] = blk + 1;
         v.need[ps] = 0;
         cnt[C_NN] += 1;
@@ -1316,10 +1356,10 @@ __device__ PlayOut play_move_choice(const View &v, int tree, double temp, float 
   constexpr int P = G::APAD;
   const size_t nb = nbase<G>(v, tree);
   const int root = v.root[tree];
-  const int cb = v.bc[nb + root];
+  const int cb = nd_c<P>(v, nb + root);
   PlayOut o{0, false, 0.0, 0};
   int n[G::A];
-  for (int j = 0; j < G::A; ++j) n[j] = cb >= 0 ? v.bn[nb + (size_t)cb * P + j] : 0;
+  for (int j = 0; j < G::A; ++j) n[j] = cb >= 0 ? nd_n<P>(v, nb + (size_t)cb * P + j) : 0;
   double t = temp;
   if (v.evaluate) t = t / 20.0;
   const double inv = 1.0 / t;
@@ -1357,15 +1397,15 @@ __device__ PlayOut play_move_choice(const View &v, int tree, double temp, float 
     o.action = a;
     o.recorded = true;
     for (int j = 0; j < G::A; ++j) probs_out[j] = (float)pr[j];
-    const int rn = v.bn[nb + root];
+    const int rn = nd_n<P>(v, nb + root);
     if (v.K > 1) {
       // q (mcts.py:59-62) with the root's virtual loss, nonzero after a leaked sim (:349-354)
-      const int rvl = v.bvl[nb + root];
-      o.q = (rn + rvl) ? (v.bw[nb + root] - (double)rvl) / (double)(rn + rvl) : 0.0;
+      const int rvl = nd_vl<P>(v, nb + root);
+      o.q = (rn + rvl) ? (nd_w<P>(v, nb + root) - (double)rvl) / (double)(rn + rvl) : 0.0;
     } else {
-      o.q = rn ? v.bw[nb + root] / (double)rn : 0.0;
+      o.q = rn ? nd_w<P>(v, nb + root) / (double)rn : 0.0;
     }
-    o.qf64 = v.bf64[nb + root];
+    o.qf64 = nd_f<P>(v, nb + root);
   } else {
     int best = 0;
     for (int j = 1; j < G::A; ++j)
@@ -1407,8 +1447,8 @@ __device__ bool set_node(const View &v, int tree, int a) {
   const size_t nb = nbase<G>(v, tree);
   const size_t bb = (size_t)tree * v.cap;
   const int root = v.root[tree];
-  const int cb = v.bc[nb + root];
-  if (cb < 0 || a < 0 || a >= G::A || !((v.bvm[bb + cb] >> a) & 1u)) {
+  const int cb = nd_c<P>(v, nb + root);
+  if (cb < 0 || a < 0 || a >= G::A || !((nd_vm<P>(v, bb + cb) >> a) & 1u)) {
     set_err(v, SPMCTS_ERR_ACTION);
     return false;
   }
@@ -1417,20 +1457,20 @@ __device__ bool set_node(const View &v, int tree, int a) {
   Board b{v.rpos[tree], v.rneg[tree]};
   int rew = 0, done = 0;
   step<G>(b, a, rp, &rew, &done);
-  if (v.bn[nb + child] == 0) {
+  if (nd_n<P>(v, nb + child) == 0) {
     int64_t *cnt = v.cnt + (size_t)tree * C_NCNT;
     cnt[C_SETNODE] += 1;
     if (done) {
       const double val = terminal_value(v, tree, Board{v.rpos[tree], v.rneg[tree]}, rew * rp);
-      v.bn[nb + child] = 1;
-      v.bw[nb + child] = v.bw[nb + child] + val;
-      if (v.tstrong[tree]) v.bf64[nb + child] = 1;
+      nd_n<P>(v, nb + child) = 1;
+      nd_w<P>(v, nb + child) = nd_w<P>(v, nb + child) + val;
+      if (v.tstrong[tree]) nd_f<P>(v, nb + child) = 1;
     } else {
       const int ps = tree * v.K;  // pending slot 0 of the tree
       v.plen[ps] = 0;
       v.leaf[ps] = child;
       v.leaf_n[ps] = 0;
-      v.leaf_w[ps] = v.bw[nb + child];
+      v.leaf_w[ps] = nd_w<P>(v, nb + child);
       v.lpos[ps] = b.pos;
       v.lneg[ps] = b.neg;
       v.lmover[ps] = (int8_t)rp;
@@ -1837,17 +1877,16 @@ struct Plan {
   }
 };
 
+// device address of a field of node i (host side; off = the field's NodeRec offset in units of P bytes)
+static const char *node_field(const spmcts_arena *h, int off, int elt, size_t i) {
+  const size_t P = h->P;
+  return h->v.nodes + (i / P) * 32 * P + off * P + (i % P) * elt;
+}
+
 static void plan_arena(spmcts_arena *h, Plan &pl) {
   View &v = h->v;
   const size_t T = v.T, P = h->P, cap = v.cap, G = v.G;
-  const size_t nodes = T * cap * P;
-  pl.add(&v.bn, nodes);
-  pl.add(&v.bw, nodes);
-  pl.add(&v.bp, nodes);
-  pl.add(&v.bc, nodes);
-  pl.add(&v.bf64, nodes);
-  pl.add(&v.bvl, v.K > 1 ? nodes : 1);
-  pl.add(&v.bvm, T * cap);
+  pl.add(&v.nodes, T * cap * 32 * P);  // 32 * P bytes per child block (NodeRec)
   pl.add(&v.root, T);
   pl.add(&v.rpos, T);
   pl.add(&v.rneg, T);
@@ -2357,18 +2396,18 @@ int spmcts_root_stats(spmcts_arena *h, int32_t tree, int32_t *child_n, double *c
   int8_t rp = 0;
   uint64_t pos = 0, neg = 0;
   HIP_TRY(hipMemcpy(&root, h->v.root + tree, 4, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(&cb, h->v.bc + nb + root, 4, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(&cb, node_field(h, 8, 4, nb + root), 4, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(&rp, h->v.rplayer + tree, 1, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(&pos, h->v.rpos + tree, 8, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(&neg, h->v.rneg + tree, 8, hipMemcpyDeviceToHost));
-  if (root_n) HIP_TRY(hipMemcpy(root_n, h->v.bn + nb + root, 4, hipMemcpyDeviceToHost));
-  if (root_w) HIP_TRY(hipMemcpy(root_w, h->v.bw + nb + root, 8, hipMemcpyDeviceToHost));
+  if (root_n) HIP_TRY(hipMemcpy(root_n, node_field(h, 0, 4, nb + root), 4, hipMemcpyDeviceToHost));
+  if (root_w) HIP_TRY(hipMemcpy(root_w, node_field(h, 16, 8, nb + root), 8, hipMemcpyDeviceToHost));
   if (root_player) *root_player = rp;
   if (cb >= 0) {
     const size_t ci = nb + (size_t)cb * h->P;
-    if (child_n) HIP_TRY(hipMemcpy(child_n, h->v.bn + ci, 4 * h->A, hipMemcpyDeviceToHost));
-    if (child_w) HIP_TRY(hipMemcpy(child_w, h->v.bw + ci, 8 * h->A, hipMemcpyDeviceToHost));
-    if (child_p) HIP_TRY(hipMemcpy(child_p, h->v.bp + ci, 4 * h->A, hipMemcpyDeviceToHost));
+    if (child_n) HIP_TRY(hipMemcpy(child_n, node_field(h, 0, 4, ci), 4 * h->A, hipMemcpyDeviceToHost));
+    if (child_w) HIP_TRY(hipMemcpy(child_w, node_field(h, 16, 8, ci), 8 * h->A, hipMemcpyDeviceToHost));
+    if (child_p) HIP_TRY(hipMemcpy(child_p, node_field(h, 12, 4, ci), 4 * h->A, hipMemcpyDeviceToHost));
   } else {
     for (int j = 0; j < h->A; ++j) {
       if (child_n) child_n[j] = 0;

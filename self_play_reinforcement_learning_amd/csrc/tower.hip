@@ -142,7 +142,8 @@ struct Cfg : Ty<E_> {
   static_assert(CG * MG == WAVES, "wave plan");
   static_assert(BOARDS >= 1, "board larger than a tile");
   static_assert(LDS <= 163840, "LDS budget");
-  static_assert(!EDGE_ || (W == 7 && H == 6 && ROWS == 256 && BOARDS == 6 && MG == 2), "edge layout: 6 Connect4 boards");
+  static_assert(!EDGE_ || (W == 7 && H == 6 && ROWS == 256 && BOARDS == 6 && (MG == 2 || MG == 1)),
+                "edge layout: 6 Connect4 boards, two row halves or one");
   // Row layout of the tile.  Board-major (default): row = board * CELLS + x * H + y.  Column-major
   // across boards (XMAJ): row = x * (BOARDS * H) + board * H + y, so each board column x of all the
   // tile's boards is BOARDS*H consecutive rows: with 6 boards (36 rows per column) cell tile 0 lies
@@ -628,7 +629,7 @@ __device__ __forceinline__ void conv_tap_x(const char *src, const Nbr<K> &nb, f3
   // weight-load cache policy (timing variants: ABL 4096 = sc0, 8192 = nt, 16384 = sc1)
   constexpr int WAUX = (K::ABL & 4096) ? 1 : (K::ABL & 8192) ? 2 : (K::ABL & 16384) ? 16 : 0;
   constexpr int NTA = (int)X::popc(LV);
-  static_assert(NTA >= 1 && K::MT * NTA >= NTA + K::MT, "schedule: enough MFMAs for the loads");
+  static_assert(NTA >= 1 && (K::MT == 1 || K::MT * NTA >= NTA + K::MT), "schedule: enough MFMAs for the loads");
   if constexpr (TAP < 8) {
     // the next tap's neighbour rows are read here, ahead of this tap's operand reads, and turned
     // into addresses only where the tap's last k-step uses them: read at the tap boundary they made
@@ -689,17 +690,30 @@ __device__ __forceinline__ void conv_tap_x(const char *src, const Nbr<K> &nb, f3
         for (int m = 0; m < K::MT; ++m)
           if ((LV >> t) & 1u) acc[m][t] = K::mfma(acur[m], bc[t], acc[m][t]);
     }
-#pragma unroll
-    for (int i = 0; i < NTA; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-    }
-#pragma unroll
-    for (int i = 0; i < K::MT; ++i) {
+    if constexpr (K::MT == 1) {
+      // one channel tile per wave (four channel quarters, no duplicate weight requests): NTA MFMAs
+      // carry the step's one weight load and its NTA operand reads, one read per gap
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
       __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+#pragma unroll
+      for (int i = 1; i < NTA; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NTA; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+      }
+#pragma unroll
+      for (int i = 0; i < K::MT; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, K::MT * NTA - NTA - K::MT, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, K::MT * NTA - NTA - K::MT, 0);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = 0; t < K::NT; ++t) bc[t] = bn[t];
@@ -827,12 +841,12 @@ __device__ __forceinline__ void conv_layer_x(const char *src, char *dst, const N
     } else {
       acc_store_bias_relu_pre<K, RESID>(acc, dst, bv, wave, lane);
     }
-    return;
+  } else {
+    conv_group_x<K, KK, DEPTH, MG_, 0>(src, nb, acc, bc, bn, off_cur, off_nxt, a, hoff, wb, wl_off, wn_off, wn_steps);
+    conv_group_x<K, KK, DEPTH, MG_, 1>(src, nb, acc, bc, bn, off_cur, off_nxt, a, hoff, wb, wl_off, wn_off, wn_steps);
+    conv_group_x<K, KK, DEPTH, MG_, 2>(src, nb, acc, bc, bn, off_cur, off_nxt, a, hoff, wb, wl_off, wn_off, wn_steps);
+    acc_store_bias_relu_pre<K, RESID>(acc, dst, bv, wave, lane);
   }
-  conv_group_x<K, KK, DEPTH, MG_, 0>(src, nb, acc, bc, bn, off_cur, off_nxt, a, hoff, wb, wl_off, wn_off, wn_steps);
-  conv_group_x<K, KK, DEPTH, MG_, 1>(src, nb, acc, bc, bn, off_cur, off_nxt, a, hoff, wb, wl_off, wn_off, wn_steps);
-  conv_group_x<K, KK, DEPTH, MG_, 2>(src, nb, acc, bc, bn, off_cur, off_nxt, a, hoff, wb, wl_off, wn_off, wn_steps);
-  acc_store_bias_relu_pre<K, RESID>(acc, dst, bv, wave, lane);
 }
 
 // Stem: 3 input planes padded to one 16-channel k-step per tap (9 steps, weights loaded in place).
@@ -946,10 +960,11 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
   if constexpr (K::EDGE) {
     uint16_t *tab = (uint16_t *)(smem + 2 * K::BUF);
     static_assert(K::ROWS == 256 && K::ZROW == 256, "EDGE_NBR is laid out for 256-row tiles");
-    static_assert(9 * K::ROWS % K::THREADS == 0, "neighbour table copy: whole rounds");
     // unrolled so all of a thread's table loads are in flight at once (a rolled loop waited for each)
 #pragma unroll
-    for (int j = 0; j < 9 * K::ROWS / K::THREADS; ++j) tab[tid + j * K::THREADS] = kEdgeNbr[tid + j * K::THREADS];
+    for (int j = 0; j < (9 * K::ROWS + K::THREADS - 1) / K::THREADS; ++j)
+      if (9 * K::ROWS % K::THREADS == 0 || tid + j * K::THREADS < 9 * K::ROWS)
+        tab[tid + j * K::THREADS] = kEdgeNbr[tid + j * K::THREADS];
     nb.tab = tab;
   }
   for (int row = tid; row < K::ROWS; row += K::THREADS) {
@@ -999,10 +1014,14 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
     }
     const int wn_steps = L + 1 < n_convs ? LSTEPS : 0;
     if constexpr (K::XMAJ) {
-      static_assert(K::MG == 2 && (K::ABL & ~(2 | 4 | 8 | 16 | 128 | 512 | 4096 | 8192 | 16384)) == 0 && (K::ABL == 0 || K::EDGE),
-                    "column-group conv: two row halves; edge tiles take the 2/4/8/16/128 timing ablations");
+      static_assert((K::MG == 2 || (K::MG == 1 && K::EDGE)) &&
+                        (K::ABL & ~(2 | 4 | 8 | 16 | 128 | 512 | 4096 | 8192 | 16384)) == 0 && (K::ABL == 0 || K::EDGE),
+                    "column-group conv: two row halves (edge tiles: or one); edge tiles take the 2/4/8/16/128 timing ablations");
       const bool even = (L & 1) == 0;
-      if (wave / K::CG == 0) {
+      if constexpr (K::MG == 1) {
+        if (even) conv_layer_x<K, KK, DEPTH, false, 0>(X, Y, nb, ring, b, wave, lane, wb, wl_off, wn_off, wn_steps);
+        else conv_layer_x<K, KK, DEPTH, true, 0>(Y, X, nb, ring, b, wave, lane, wb, wl_off, wn_off, wn_steps);
+      } else if (wave / K::CG == 0) {
         if (even) conv_layer_x<K, KK, DEPTH, false, 0>(X, Y, nb, ring, b, wave, lane, wb, wl_off, wn_off, wn_steps);
         else conv_layer_x<K, KK, DEPTH, true, 0>(Y, X, nb, ring, b, wave, lane, wb, wl_off, wn_off, wn_steps);
       } else {
@@ -1556,6 +1575,12 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
       case 302: return launch<Cfg<128, 256, 7, 6, 2, 4, 8192, 4, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       case 316: return launch<Cfg<128, 256, 7, 6, 2, 4, 16384, 4, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
 #undef ABLATE_EDGE
+      // four channel quarters x one row group (each wave all 8 cell tiles, one weight fragment per k-step)
+      case 400: return launch<Cfg<128, 256, 7, 6, 4, 4, 0, 4, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      case 408: return launch<Cfg<128, 256, 7, 6, 4, 4, 0, 8, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      // eight waves (two per SIMD): four channel quarters x two row halves, one weight fragment per k-step
+      case 800: return launch<Cfg<128, 256, 7, 6, 4, 8, 0, 4, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      case 808: return launch<Cfg<128, 256, 7, 6, 4, 8, 0, 8, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       case 250: return launch<Cfg<128, 256, 7, 6, 2, 4, 0, 8, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);  // ring depth 8
       case 10: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);  // two tile sizes only
       case 15: return launch_split<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true>, Cfg<128, 192, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);  // column-major tiles without edge rows
