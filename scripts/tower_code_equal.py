@@ -1,6 +1,6 @@
 """Bit-equality of a timing alternative (SPMCTS_TOWER_CG) with the default trunk: run once per code
 (the switch is read once per process) writing the host-path outputs, then compare the files.
-  python scripts/tower_code_equal.py dump OUT.npz   |   python scripts/tower_code_equal.py cmp A.npz B.npz"""
+  python scripts/tower_code_equal.py dump OUT.npz [FILTER_FACTOR]   |   python scripts/tower_code_equal.py cmp A.npz B.npz"""
 import sys
 
 import os
@@ -10,7 +10,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def dump(out):
+def dump(out, ff=32):
     import torch
 
     from self_play_reinforcement_learning_amd.evaluator import HipTowerEvaluator
@@ -19,7 +19,7 @@ def dump(out):
     res = {}
     for blocks in (2, 20):
         torch.manual_seed(0)
-        net = ResidualTower(7, 6, 7, num_blocks=blocks, filter_factor=32)
+        net = ResidualTower(7, 6, 7, num_blocks=blocks, filter_factor=ff)
         with torch.no_grad():
             for m in net.modules():
                 if isinstance(m, torch.nn.BatchNorm2d):
@@ -29,9 +29,16 @@ def dump(out):
         b = np.random.default_rng(1).choice([-1, 0, 1], size=(4000, 7, 6), p=[0.3, 0.4, 0.3])
         x = planes_from_boards(torch.as_tensor(b), 7, 6).cuda()
         x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        p, v = HipTowerEvaluator(net)(x)
+        ev = HipTowerEvaluator(net)
+        p, v = ev(x)
         res[f"p{blocks}"] = p.float().cpu().numpy()
         res[f"v{blocks}"] = v.float().cpu().numpy()
+        # the device-count path (k_tower_dyn) on a ragged batch: whole rounds + tail tiles
+        n = 3001
+        cnt = torch.tensor([n], dtype=torch.int32, device="cuda")
+        pd, vd = ev.forward_dev(x, cnt, 4000)
+        res[f"pd{blocks}"] = pd[:n].float().cpu().numpy()
+        res[f"vd{blocks}"] = vd[:n].float().cpu().numpy()
     np.savez(out, **res)
 
 
@@ -45,6 +52,6 @@ def cmp(a, b):
 
 if __name__ == "__main__":
     if sys.argv[1] == "dump":
-        dump(sys.argv[2])
+        dump(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 32)
     else:
         sys.exit(cmp(sys.argv[2], sys.argv[3]))

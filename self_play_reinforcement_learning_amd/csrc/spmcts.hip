@@ -736,11 +736,17 @@ enum { SIM_DONE = 0, SIM_PENDING = 1, SIM_LEAK = 2, SIM_ERROR = -1 };
 
 // The searching tree's root, loaded once per kernel and kept in registers across the K fills /
 // backups / refills (it is on every path): node id, its child block (fixed during a search: the
-// root is expanded), board, player, and its visit count and virtual loss, updated in step with the
-// stores every sim and backup makes to them.
+// root is expanded), board, player, and its visit count and virtual loss — and its child block
+// (lane j < A: child j's n, w, p, child index, vl; the valid mask), the first level every sim
+// scores.  Every store a sim or backup makes to these nodes is made to the registers as well (the
+// same arithmetic), so depth 0 reads no memory.
 struct TreeRoot {
   int node, cb, player, n, vl;
   Board b;
+  int cn, cc, cvl;
+  double cw;
+  float cp;
+  uint32_t vm;
 };
 
 template <class G>
@@ -754,6 +760,24 @@ __device__ __forceinline__ TreeRoot load_root(const View &v, int tree) {
   R.n = nd_n<P>(v, nb + R.node);
   R.vl = nd_vl<P>(v, nb + R.node);
   R.cb = nd_c<P>(v, nb + R.node);
+  const int lane = threadIdx.x & (P - 1);
+  R.cn = 0;
+  R.cc = -1;
+  R.cvl = 0;
+  R.cw = 0.0;
+  R.cp = 0.f;
+  R.vm = 0u;
+  if (R.cb >= 0) {
+    R.vm = nd_vm<P>(v, (size_t)tree * v.cap + R.cb);
+    if (lane < G::A) {
+      const size_t ci = nb + (size_t)R.cb * P + lane;
+      R.cn = nd_n<P>(v, ci);
+      R.cw = nd_w<P>(v, ci);
+      R.cp = nd_p<P>(v, ci);
+      R.cc = nd_c<P>(v, ci);
+      R.cvl = nd_vl<P>(v, ci);
+    }
+  }
   return R;
 }
 
@@ -781,26 +805,38 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
   int cb = R.cb;
   R.vl += 1;
   int depth = 0;
+  int a0 = 0;  // the root child this sim took (path node 1)
   for (;;) {
     if (lane == 0) {
       s_node[depth] = node;
       nd_vl<P>(v, nb + node) = node_vl;
     }
+    if (depth == 1 && lane == a0) R.cvl = node_vl;  // the root child's vl, in registers too
     if (cb < 0) {
       if (lane == 0) set_err(v, SPMCTS_ERR_STATE);
       return SIM_ERROR;
     }
-    const uint32_t vm = nd_vm<P>(v, bb + cb);
-    const size_t ci = nb + (size_t)cb * P + lane;
+    uint32_t vm;
     int cn = 0, cc = -1, cvl = 0;
     double cw = 0.0;
     float cp = 0.f;
-    if (lane < G::A) {
-      cn = nd_n<P>(v, ci);
-      cw = nd_w<P>(v, ci);
-      cp = nd_p<P>(v, ci);
-      cc = nd_c<P>(v, ci);
-      cvl = nd_vl<P>(v, ci);
+    if (depth == 0) {  // the root's child block, from registers
+      vm = R.vm;
+      cn = R.cn;
+      cw = R.cw;
+      cp = R.cp;
+      cc = R.cc;
+      cvl = R.cvl;
+    } else {
+      vm = nd_vm<P>(v, bb + cb);
+      const size_t ci = nb + (size_t)cb * P + lane;
+      if (lane < G::A) {
+        cn = nd_n<P>(v, ci);
+        cw = nd_w<P>(v, ci);
+        cp = nd_p<P>(v, ci);
+        cc = nd_c<P>(v, ci);
+        cvl = nd_vl<P>(v, ci);
+      }
     }
     // the jitter does not depend on the child block: drawn here, it overlaps the loads above
     bool terr_j = false;
@@ -855,6 +891,15 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
         }
         R.n += 1;  // the root is s_node[0]
         R.vl -= 1;
+        if (depth >= 1 && lane == a0) {  // path node 1, the root child a0
+          R.cn += 1;
+          R.cw += val;
+          R.cvl -= 1;
+        }
+        if (depth == 0 && lane == a) {  // the terminal leaf is a root child
+          R.cn += 1;
+          R.cw += val;
+        }
       } else {
         const size_t pb = (size_t)ps * G::MAXD;
         for (int k = lane; k <= depth; k += P) v.pnode[pb + k] = s_node[k];
@@ -876,8 +921,10 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
           v.need[ps] = 1;
         }
       }
+      if (!done && depth == 0 && lane == a) R.cc = -2;
       return done ? SIM_DONE : SIM_PENDING;
     }
+    if (depth == 0) a0 = a;
     play<G>(b, a, player);
     node = child;
     node_n = cn_a;
@@ -1315,6 +1362,19 @@ __device__ __forceinline__ void expand_vl_body(View v, const float *probs0, cons
       if (refill && plen > 0) {  // the root is the path's first node
         R.n += 1;
         R.vl -= 1;
+      }
+      if (refill && plen > 1) {  // path node 1 is a root child: its copy in registers
+        if (lane == s_pnode[grp][j][1] - R.cb * P) {
+          R.cn += 1;
+          R.cw += val;
+          R.cvl -= 1;
+        }
+      } else if (refill && plen == 1) {  // the leaf itself is a root child
+        if (lane == leaf - R.cb * P) {
+          R.cc = blk;
+          R.cn += 1;
+          R.cw += val;
+        }
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
       if (refill &&

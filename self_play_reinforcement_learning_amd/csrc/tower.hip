@@ -24,7 +24,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
 #include <utility>
+#include <vector>
 
 #include "spmcts.h"
 #include "tower_edge.h"
@@ -101,7 +103,7 @@ struct Ty<_Float16> {
 
 
 template <int C_, int ROWS_, int W_, int H_, int CG_ = 2, int WAVES_ = 4, int ABL_ = 0, int DEPTH_ = 4, int OCC_ = 1,
-          bool XMAJ_ = false, bool EDGE_ = false, class E_ = __bf16>
+          bool XMAJ_ = false, bool EDGE_ = false, class E_ = __bf16, bool ONEBUF_ = false>
 struct Cfg : Ty<E_> {
   using E = E_;  // operand / activation element type (Ty)
   static constexpr int OCC = OCC_;  // resident workgroups per CU the register budget is sized for
@@ -135,10 +137,12 @@ struct Cfg : Ty<E_> {
   // a 9 x ROWS table of neighbour rows (zero rows for off-board) sits in LDS after the buffers.
   static constexpr bool EDGE = EDGE_ && XMAJ_;
   static constexpr int TAB = EDGE ? 9 * ROWS * 2 : 0;
-  static constexpr int LDS = 2 * BUF + TAB;
+  // ONEBUF (tower_wide.h): one activation buffer, convs in place between two barriers
+  static constexpr bool ONEBUF = ONEBUF_;
+  static constexpr int LDS = (ONEBUF ? 1 : 2) * BUF + TAB;
   static constexpr int HEAD = C / 2;  // policy filter_factor | value filter_factor channels (filter_factor = C/4)
   static constexpr int HCT = HEAD / 32;  // head channel tiles
-  static_assert(MT >= 1 && NT >= 1 && MT * NT <= 8, "tile plan: at most 8 accumulator tiles per wave");
+  static_assert(MT >= 1 && NT >= 1 && MT * NT <= (ONEBUF_ ? 16 : 8), "tile plan: at most 8 (one buffer: 16) accumulator tiles per wave");
   static_assert(CG * MG == WAVES, "wave plan");
   static_assert(BOARDS >= 1, "board larger than a tile");
   static_assert(LDS <= 163840, "LDS budget");
@@ -943,9 +947,15 @@ __device__ __forceinline__ void head_layer(const char *src, const bf16x8 *w, con
 // lane l of fragment (ct, tap, kk) holds W[ct*32 + (l & 31)][tap][kk*16 + 8*(l >> 5) + j], j = 0..7.
 // bias: stem C, blocks 2*C each, head C/2.
 // One workgroup's tile: boards [board0, board0 + BOARDS) of the batch (board < batch), all layers.
+#include "tower_wide.h"
+
 template <class K>
 __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int batch, int board0, int n_blocks,
-                                           const bf16x8 *wpk, const float *bias, uint16_t *out) {
+                                           const bf16x8 *wpk, const float *bias, uint16_t *out, uint4 *scr) {
+  if constexpr (K::ONEBUF) {
+    wide::tile<K>(smem, planes, batch, board0, n_blocks, wpk, bias, out, scr + blockIdx.x * (wide::Scr<K>::PER_WG / 16));
+    return;
+  }
   char *X = smem;
   char *Y = smem + K::BUF;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1044,9 +1054,9 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
 
 template <class K>
 __global__ __launch_bounds__(K::THREADS) __attribute__((amdgpu_waves_per_eu(K::WAVES / 4 * K::OCC, K::WAVES / 4 * K::OCC))) void k_tower(
-    const __bf16 *planes, int batch, int n_blocks, const bf16x8 *wpk, const float *bias, uint16_t *out) {
+    const __bf16 *planes, int batch, int n_blocks, const bf16x8 *wpk, const float *bias, uint16_t *out, uint4 *scr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  tower_tile<K>(smem, planes, batch, blockIdx.x * K::BOARDS, n_blocks, wpk, bias, out);
+  tower_tile<K>(smem, planes, batch, blockIdx.x * K::BOARDS, n_blocks, wpk, bias, out, scr);
 }
 
 // Tail tile for a remainder of `rem` boards after whole rounds of full tiles: the smallest tile
@@ -1066,8 +1076,9 @@ __host__ __device__ __forceinline__ int tail_kind(int rem, int cus) {
 template <class KF, class KM, class KH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_tower_dyn(
     const __bf16 *planes, const int32_t *count, int max_batch, int cus, int n_blocks, const bf16x8 *wpk,
-    const float *bias, uint16_t *out) {
+    const float *bias, uint16_t *out, uint4 *scr) {
   static_assert(KF::THREADS == 256 && KM::THREADS == 256 && KH::THREADS == 256, "one block size");
+  static_assert(!KM::ONEBUF && !KH::ONEBUF, "residual scratch is sized for the full tiles only");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int n = min(*count, max_batch);  // never past the caller's buffers
   const int full_wgs = (n / KF::BOARDS) / cus * cus;
@@ -1075,17 +1086,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int rem = n - n_full;
   const int b = blockIdx.x;
   if (b < full_wgs) {
-    tower_tile<KF>(smem, planes, n, b * KF::BOARDS, n_blocks, wpk, bias, out);
+    tower_tile<KF>(smem, planes, n, b * KF::BOARDS, n_blocks, wpk, bias, out, scr);
     return;
   }
   const int j = b - full_wgs;
   const int kind = tail_kind<KF, KM, KH>(rem, cus);
   if (kind == 0) {
-    if (n_full + j * KH::BOARDS < n) tower_tile<KH>(smem, planes, n, n_full + j * KH::BOARDS, n_blocks, wpk, bias, out);
+    if (n_full + j * KH::BOARDS < n) tower_tile<KH>(smem, planes, n, n_full + j * KH::BOARDS, n_blocks, wpk, bias, out, scr);
   } else if (kind == 1) {
-    if (n_full + j * KM::BOARDS < n) tower_tile<KM>(smem, planes, n, n_full + j * KM::BOARDS, n_blocks, wpk, bias, out);
+    if (n_full + j * KM::BOARDS < n) tower_tile<KM>(smem, planes, n, n_full + j * KM::BOARDS, n_blocks, wpk, bias, out, scr);
   } else {
-    if (n_full + j * KF::BOARDS < n) tower_tile<KF>(smem, planes, n, n_full + j * KF::BOARDS, n_blocks, wpk, bias, out);
+    if (n_full + j * KF::BOARDS < n) tower_tile<KF>(smem, planes, n, n_full + j * KF::BOARDS, n_blocks, wpk, bias, out, scr);
   }
 }
 
@@ -1375,11 +1386,48 @@ __global__ __launch_bounds__(256) void k_head_epilogue(const __bf16 *Z, int ldz,
   if (lane == 0) values[wave] = tanhf(acc + bo[0]);
 }
 
+// Residual scratch of the one-buffer trunk (tower_wide.h): one region per workgroup of a launch, one
+// buffer per stream (launches on different streams run concurrently), grown on demand.
+static uint4 *wide_scratch(hipStream_t s, size_t bytes) {
+  struct Ent {
+    hipStream_t s;
+    void *p;
+    size_t n;
+  };
+  static std::vector<Ent> tab;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lk(mu);
+  for (auto &e : tab)
+    if (e.s == s) {
+      if (e.n >= bytes) return (uint4 *)e.p;
+      if (hipStreamSynchronize(s) != hipSuccess || hipFree(e.p) != hipSuccess) return nullptr;
+      e.p = nullptr;
+      e.n = 0;
+      if (hipMalloc(&e.p, bytes) != hipSuccess) return nullptr;
+      e.n = bytes;
+      return (uint4 *)e.p;
+    }
+  void *p = nullptr;
+  if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+  tab.push_back({s, p, bytes});
+  return (uint4 *)p;
+}
+
+template <class K>
+static size_t scratch_bytes(int grid) {
+  if constexpr (K::ONEBUF) return (size_t)grid * wide::Scr<K>::PER_WG;
+  return 0;
+}
+
 template <class K>
 static int launch(const void *planes, int batch, int n_blocks, const void *w, const float *b, void *out,
                   hipStream_t s) {
   const int grid = (batch + K::BOARDS - 1) / K::BOARDS;
   if (grid <= 0) return 0;
+  uint4 *scr = nullptr;
+  if (const size_t sb = scratch_bytes<K>(grid)) {
+    if (!(scr = wide_scratch(s, sb))) return -12;
+  }
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void *)k_tower<K>, hipFuncAttributeMaxDynamicSharedMemorySize, K::LDS) !=
@@ -1388,7 +1436,7 @@ static int launch(const void *planes, int batch, int n_blocks, const void *w, co
     attr_set = true;
   }
   hipLaunchKernelGGL(k_tower<K>, dim3(grid), dim3(K::THREADS), K::LDS, s, (const __bf16 *)planes, batch, n_blocks,
-                     (const bf16x8 *)w, b, (uint16_t *)out);
+                     (const bf16x8 *)w, b, (uint16_t *)out, scr);
   return hipGetLastError() == hipSuccess ? 0 : -11;
 }
 
@@ -1434,6 +1482,10 @@ static int launch_dyn(const void *planes, const int32_t *count, int max_batch, i
                       const float *b, void *out, bool pack, hipStream_t s) {
   const int cus = pack ? 1 : num_cus();
   const int grid = (max_batch + KF::BOARDS - 1) / KF::BOARDS + (pack ? 1 : cus);
+  uint4 *scr = nullptr;
+  if (const size_t sb = scratch_bytes<KF>(grid)) {  // (the tail kinds KM / KH are two-buffer tiles)
+    if (!(scr = wide_scratch(s, sb))) return -12;
+  }
   constexpr int LDS = KF::LDS > KM::LDS ? (KF::LDS > KH::LDS ? KF::LDS : KH::LDS) : (KM::LDS > KH::LDS ? KM::LDS : KH::LDS);
   static bool attr_set = false;
   if (!attr_set) {
@@ -1443,13 +1495,24 @@ static int launch_dyn(const void *planes, const int32_t *count, int max_batch, i
     attr_set = true;
   }
   hipLaunchKernelGGL((k_tower_dyn<KF, KM, KH>), dim3(grid), dim3(256), LDS, s, (const __bf16 *)planes, count,
-                     max_batch, cus, n_blocks, (const bf16x8 *)w, b, (uint16_t *)out);
+                     max_batch, cus, n_blocks, (const bf16x8 *)w, b, (uint16_t *)out, scr);
   return hipGetLastError() == hipSuccess ? 0 : -11;
 }
 
 }  // namespace tower
 
 namespace tower {
+// The C = 256 trunk runs on 3-board two-buffer tiles unless SPMCTS_TOWER_C256=6 selects the 6-board
+// one-buffer tiles (tower_wide.h: bit-identical outputs, measured no faster).  Read once.
+static bool c256_board3() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("SPMCTS_TOWER_C256");
+    v = !(e && atoi(e) == 6);
+  }
+  return v != 0;
+}
+
 // the instantiated tile sets of the device-count path, per board shape, channels and element type
 template <class E>
 static int forward_dev(int32_t width, int32_t height, int32_t channels, int32_t n_blocks, const void *planes_dev,
@@ -1459,10 +1522,14 @@ static int forward_dev(int32_t width, int32_t height, int32_t channels, int32_t 
     return launch_dyn<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true, true, E>, Cfg<128, 192, 7, 6, 2, 4, 0, 4, 1, false, false, E>,
                       Cfg<128, 128, 7, 6, 2, 4, 0, 4, 1, false, false, E>>(planes_dev, count_dev, max_batch, n_blocks,
                                                                           weights_dev, bias_dev, features_dev, pack, s);
-  if (width == 7 && height == 6 && channels == 256)
-    return launch_dyn<Cfg<256, 128, 7, 6, 4, 4, 0, 4, 1, false, false, E>, Cfg<256, 128, 7, 6, 4, 4, 0, 4, 1, false, false, E>,
-                      Cfg<256, 128, 7, 6, 4, 4, 0, 4, 1, false, false, E>>(planes_dev, count_dev, max_batch, n_blocks,
-                                                                          weights_dev, bias_dev, features_dev, pack, s);
+  if (width == 7 && height == 6 && channels == 256) {
+    // 3-board two-buffer tiles; SPMCTS_TOWER_C256=6: 6-board one-buffer edge tiles (tower_wide.h), 3-board tails
+    using K3 = Cfg<256, 128, 7, 6, 4, 4, 0, 4, 1, false, false, E>;
+    if (c256_board3())
+      return launch_dyn<K3, K3, K3>(planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, pack, s);
+    return launch_dyn<Cfg<256, 256, 7, 6, 4, 4, 0, 4, 1, true, true, E, true>, K3, K3>(
+        planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, pack, s);
+  }
   if (width == 3 && height == 3 && channels == 128)
     return launch_dyn<Cfg<128, 256, 3, 3, 2, 4, 0, 4, 1, false, false, E>, Cfg<128, 192, 3, 3, 2, 4, 0, 4, 1, false, false, E>,
                       Cfg<128, 128, 3, 3, 2, 4, 0, 4, 1, false, false, E>>(planes_dev, count_dev, max_batch, n_blocks,
@@ -1545,8 +1612,12 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
     if (width == 7 && height == 6 && channels == 128)
       return launch_split<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true, true, E>, Cfg<128, 192, 7, 6, 2, 4, 0, 4, 1, false, false, E>,
                           Cfg<128, 128, 7, 6, 2, 4, 0, 4, 1, false, false, E>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-    if (width == 7 && height == 6 && channels == 256)
-      return launch<Cfg<256, 128, 7, 6, 4, 4, 0, 4, 1, false, false, E>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+    if (width == 7 && height == 6 && channels == 256) {
+      using K3 = Cfg<256, 128, 7, 6, 4, 4, 0, 4, 1, false, false, E>;
+      if (c256_board3()) return launch<K3>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      return launch_split<Cfg<256, 256, 7, 6, 4, 4, 0, 4, 1, true, true, E, true>, K3, K3>(pl, batch, n_blocks,
+                                                                                         weights_dev, bias_dev, ft, s);
+    }
     if (width == 3 && height == 3 && channels == 128)
       return launch<Cfg<128, 256, 3, 3, 2, 4, 0, 4, 1, false, false, E>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
     if (width == 3 && height == 3 && channels == 256)
@@ -1588,8 +1659,12 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
       default: return launch_split<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true, true>, Cfg<128, 192, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
     }
   }
-  if (width == 7 && height == 6 && channels == 256)
-    return launch<Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);  // as the device-count path
+  if (width == 7 && height == 6 && channels == 256) {  // as the device-count path
+    using K3 = Cfg<256, 128, 7, 6, 4>;
+    if (c256_board3()) return launch<K3>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+    return launch_split<Cfg<256, 256, 7, 6, 4, 4, 0, 4, 1, true, true, __bf16, true>, K3, K3>(pl, batch, n_blocks,
+                                                                                          weights_dev, bias_dev, ft, s);
+  }
   if (width == 3 && height == 3 && channels == 128)
     return launch<Cfg<128, 256, 3, 3>>(planes_dev, batch, n_blocks, weights_dev, bias_dev, features_dev, s);
   if (width == 3 && height == 3 && channels == 256)

@@ -230,3 +230,40 @@ def test_ring_trunk_variant():
     res = json.loads(r.stdout.strip().splitlines()[-1])
     for dt, d in res.items():
         assert d["err"] < 0.05 and d["dev_equal"] and d["batch_equal"], (dt, d)
+
+
+_WIDE_CHILD = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+from tests.test_gpu_tower import _net, _planes
+from self_play_reinforcement_learning_amd.evaluator import HipTowerEvaluator
+out = {}
+for dt, name in ((torch.bfloat16, "bf16"), (torch.float16, "fp16")):
+    hip = HipTowerEvaluator(_net(7, 6, 7, 3, 64), dtype=dt)
+    x = _planes(7, 6, 1601).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    p, v = hip(x)
+    out["p" + name], out["v" + name] = p.float().cpu().numpy(), v.float().cpu().numpy()
+    cnt = torch.tensor([1000], dtype=torch.int32, device="cuda")
+    pd, vd = hip.forward_dev(x, cnt, 1601)
+    out["pd" + name], out["vd" + name] = pd[:1000].float().cpu().numpy(), vd[:1000].float().cpu().numpy()
+np.savez(sys.argv[2], **out)
+"""
+
+
+def test_wide_c256_tiles_bit_identical(tmp_path):
+    """The one-buffer 6-board C = 256 trunk (tower_wide.h, SPMCTS_TOWER_C256=6, read once per process)
+    gives every board the same bits as the default 3-board tiles: host batch (full tiles + tails) and
+    the device-count path on a ragged batch, bf16 and fp16."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = {}
+    for tiles in ("3", "6"):
+        env = dict(os.environ, SPMCTS_TOWER_C256=tiles)
+        out = tmp_path / f"c{tiles}.npz"
+        subprocess.run([sys.executable, "-c", _WIDE_CHILD, root, str(out)], env=env, check=True, timeout=300)
+        res[tiles] = np.load(out)
+    for k in res["3"].files:
+        assert np.array_equal(res["3"][k], res["6"][k]), k
