@@ -42,8 +42,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 TRAFFIC_FILE = os.path.join(HERE, "profiles", "r01_bench_prof", "k_tower_traffic.json")  # --search-threads 1
-TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r02_bench_prof_k4", "k_tower_traffic.json")  # 4 (default)
-TREE_TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r02_tree_pmc", "tree_traffic.json")
+TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r03_bench_prof", "k_tower_traffic.json")  # 4 (default)
+TREE_TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r03_tree_pmc", "tree_traffic.json")
 
 # MI355X reference figures (/opt/skills/guides/MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0

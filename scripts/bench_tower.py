@@ -17,6 +17,7 @@ ap.add_argument("--ff", type=int, default=32)
 ap.add_argument("--blocks", type=int, default=20)
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--trunk-only", action="store_true")
+ap.add_argument("--dtype", choices=["bf16", "fp16"], default="bf16", help="the fused trunk's element type")
 args = ap.parse_args()
 torch.manual_seed(0)
 net = ResidualTower(7, 6, 7, num_blocks=args.blocks, filter_factor=args.ff).cuda().eval()
@@ -25,7 +26,7 @@ x = planes_from_boards(b, 7, 6).cuda().to(torch.bfloat16).contiguous(memory_form
 fl = resnet_flops_per_leaf(7, 6, 7, args.ff, args.blocks) * args.batch
 out = {}
 if args.trunk_only:
-    ev = HipTowerEvaluator(net)
+    ev = HipTowerEvaluator(net, dtype={"bf16": torch.bfloat16, "fp16": torch.float16}[args.dtype])
     xt = x.permute(0, 2, 3, 1)
     for _ in range(3):
         ev.trunk(xt)
@@ -37,7 +38,7 @@ if args.trunk_only:
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / args.iters
-    print(json.dumps(dict(batch=args.batch, cg=os.environ.get("SPMCTS_TOWER_CG"), trunk_ms=ms,
+    print(json.dumps(dict(batch=args.batch, dtype=args.dtype, cg=os.environ.get("SPMCTS_TOWER_CG"), trunk_ms=ms,
                           tflops=fl / ms / 1e9)))
     sys.exit(0)
 for name, ev in (("hip", HipTowerEvaluator(net)), ("hip_fusedheads", HipTowerEvaluator(net, fused_heads=True)),

@@ -4,7 +4,10 @@
 set -u
 mkdir -p gpurun_out/util
 export TMPDIR=/tmp
-timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_MFMA --kernel-include-regex "k_tower" -f csv -d gpurun_out/util/p1 -o run -- \
-  python3 scripts/bench_tower.py --trunk-only --iters 10 --batch 1536 > gpurun_out/util/p1.json 2> gpurun_out/util/p1.err
-rc=$?; echo "pmc rc=$rc"; if [ $rc -ne 0 ]; then tail -5 gpurun_out/util/p1.err; exit $rc; fi
-python3 scripts/tower_util.py gpurun_out/util/p1/run_counter_collection.csv gpurun_out/util/tower_util.json
+# DTYPES="bf16 fp16": one pass per element type of the trunk (BATCH boards per launch, default 1,536)
+for dt in ${DTYPES:-bf16}; do
+timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_MFMA --kernel-include-regex "k_tower" -f csv -d gpurun_out/util/p_$dt -o run -- \
+  python3 scripts/bench_tower.py --trunk-only --iters 10 --batch ${BATCH:-1536} --dtype $dt > gpurun_out/util/p_$dt.json 2> gpurun_out/util/p_$dt.err
+rc=$?; echo "pmc $dt rc=$rc"; if [ $rc -ne 0 ]; then tail -5 gpurun_out/util/p_$dt.err; exit $rc; fi
+python3 scripts/tower_util.py gpurun_out/util/p_$dt/run_counter_collection.csv gpurun_out/util/tower_util_$dt.json
+done
