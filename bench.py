@@ -465,7 +465,8 @@ def main():
             "nn_ms": nn_ms,
             "share_of_step": nn_ms / 1e3 / elapsed if elapsed else None,
         },
-        "exchange": {"every_plies": args.exchange_every, "rounds": ex.rounds, "rows_to_rank0": ex.rows_gathered,
+        "exchange": {"backend": torch.distributed.get_backend() if D.is_distributed() else None,
+                     "every_plies": args.exchange_every, "rounds": ex.rounds, "rows_to_rank0": ex.rows_gathered,
                      "ms_per_round": ex.seconds / max(1, ex.rounds) * 1e3,
                      "share_of_timed_region": ex.seconds / elapsed if elapsed else None},
         "tree": {

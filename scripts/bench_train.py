@@ -5,7 +5,8 @@ Workload: BASELINE configs[1] (Connect4, 200 sims, 4,096 games, ResNet-128x20, K
 the reference's trainer settings (batch 64, SGD lr 0.001 momentum 0.9 wd 1e-4, min_memory 20,000,
 memory 200,000).  The replay ring is first filled past min_memory (untimed), then --plies plies are
 timed with the trainer stepping, with its steps on their own stream (overlap, the default) or on the
-arena's stream (--no-overlap), and once with updates_per_ply = 0 for the self-play-only rate.
+arena's stream, under fp16 autocast (the UpdateWorker's, the default) or in fp32, and once with
+updates_per_ply = 0 for the self-play-only rate.
 
     python scripts/bench_train.py [--plies 24] [--updates 4]   -> one JSON line
 """
@@ -18,7 +19,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def run(args, updates, overlap):
+def run(args, updates, overlap, autocast=True):
     import torch
 
     from self_play_reinforcement_learning_amd import Connect4Env, MCTreeSearch, ModelContainer, SelfPlayScheduler
@@ -29,6 +30,7 @@ def run(args, updates, overlap):
     kw = dict(iterations=args.sims, env=Connect4Env, batch_size=64, memory_size=200000, min_memory=args.min_memory)
     sp = SelfPlayScheduler(ModelContainer(MCTreeSearch, policy_kwargs=kw), Connect4Env, network=net, save_dir=None,
                            n_games=args.games, updates_per_ply=updates, overlap_training=overlap, evaluation_games=0,
+                           train_autocast=autocast,
                            lr=0.001)
     sp.setup_player_workers()
     sp.setup_update_worker()
@@ -54,7 +56,7 @@ def run(args, updates, overlap):
     dt = time.perf_counter() - t0
     moves, steps = eng.counters()["moves"] - m0, tr.steps - s0
     loss = float(tr.last_loss) if tr.last_loss is not None else None
-    return dict(updates_per_ply=updates, trainer_stream=overlap, plies=args.plies, seconds=dt,
+    return dict(updates_per_ply=updates, trainer_stream=overlap, train_autocast=autocast, plies=args.plies, seconds=dt,
                 positions_per_s=moves / dt, sgd_steps=steps, sgd_steps_per_s=steps / dt, fill_plies=fill_plies,
                 replay_rows=len(tr.memory), last_loss=loss)
 
@@ -68,8 +70,10 @@ def main():
     ap.add_argument("--min-memory", type=int, default=20000)
     args = ap.parse_args()
     out = dict(workload=f"connect4 self-play + training, {args.sims} sims, {args.games} games, ResNet-128x20 (bf16 "
-                        f"trunk for leaves, fp32 SGD batch 64), K = 4, two lanes",
-               runs=[run(args, args.updates, True), run(args, args.updates, False), run(args, 0, True)])
+                        f"trunk for leaves, SGD batch 64 under fp16 autocast as updateworker.py:148, or fp32), K = 4, two lanes",
+               runs=[run(args, args.updates, True), run(args, args.updates, False),
+                     run(args, args.updates, True, autocast=False), run(args, args.updates, False, autocast=False),
+                     run(args, 0, True)])
     print(json.dumps(out), flush=True)
 
 

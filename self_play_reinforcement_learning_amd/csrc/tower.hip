@@ -1244,10 +1244,16 @@ __global__ __launch_bounds__(256) void k_heads(const uint16_t *feats, int n, con
 // per workgroup, half the weight traffic of 16), keeps only the cross-wave sums in LDS (4.6 KB), and
 // is held to 96 registers per lane, so one wave fits on each SIMD beside a trunk wave.  Same math
 // in the same order as k_heads (per-wave k order, fixed-order cross-wave sums): bit-identical.
-template <int FF, int CELLS, int A, class E = __bf16>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_heads_co(
+//
+// C = 256 (FF = 64: 4 value tiles per wave, which spill at 96 registers in one pass) runs the value
+// tiles in two passes of 2 over all of K (the features are read twice, from L2) within the same 96
+// registers; the C = 256 trunk wave uses 400 of a SIMD's 512, so one heads wave fits beside it.
+// part[] still sums the tiles in order 0..3: bit-identical.
+template <int FF, int CELLS, int A, class E = __bf16, int WPE = 5, int VP = HeadsCfg<FF, CELLS, A>::VTW>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_heads_co(
     const uint16_t *feats, int n, const int32_t *count, const bf16x8 *wf, const float *hb, float *probs, float *values) {
   using H = HeadsCfg<FF, CELLS, A>;
+  static_assert(H::VTW % VP == 0, "value tiles per pass");
   constexpr int BOARDS = 32;
   if (count) n = min(*count, n);  // n = the caller's buffer rows
   const int b0 = blockIdx.x * BOARDS;
@@ -1262,51 +1268,54 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
   const char *frow = (const char *)feats + (size_t)(b0 + min(r, nb - 1)) * H::FROW;
   // value tiles first, then the policy quarter (each in k_heads' per-wave k order): only one set of
   // accumulators is live at a time, which keeps the wave inside 96 registers without spills
-  f32x16 acc[H::VTW];
-#pragma unroll
-  for (int v = 0; v < H::VTW; ++v) acc[v] = f32x16{};
-  constexpr int D = 2;  // weight ring depth
-  bf16x8 ring[D][H::VTW];
-  const bf16x8 *wv = wf + (size_t)(1 + wave * H::VTW) * H::KS * 64 + lane;
   const bf16x8 *wp = wf + lane;
   const int q0 = wave * H::KQ, q1 = min(H::KS, q0 + H::KQ);
-#pragma unroll
-  for (int d = 0; d < D; ++d)
-#pragma unroll
-    for (int v = 0; v < H::VTW; ++v) ring[d][v] = wv[((size_t)v * H::KS + d) * 64];
   // the features of step s (value half at FF, policy half at 0), one step ahead
   auto feat = [&](int s, int half) {
     const int k0 = 16 * s + 8 * h;
     return *(const bf16x8 *)(frow + ((k0 / FF) * 2 * FF + half + k0 % FF) * 2);
   };
-  bf16x8 avn = feat(0, FF);
-  for (int s0 = 0; s0 < H::KS; s0 += D) {
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      const int s = s0 + d;
-      if (s >= H::KS) break;
-      const bf16x8 av = avn;
-      if (s + 1 < H::KS) avn = feat(s + 1, FF);
-      bf16x8 wcur[H::VTW];
-#pragma unroll
-      for (int v = 0; v < H::VTW; ++v) {
-        wcur[v] = ring[d][v];
-        if (s + D < H::KS) ring[d][v] = wv[((size_t)v * H::KS + s + D) * 64];
-      }
-#pragma unroll
-      for (int v = 0; v < H::VTW; ++v) acc[v] = Ty<E>::mfma(av, wcur[v], acc[v]);
-    }
-  }
-  // value: relu(acc + bv[col]) * wo[col], summed over the hidden units (cols); as k_heads
   float part[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) part[i] = 0.f;
+#pragma unroll 1
+  for (int v0 = 0; v0 < H::VTW; v0 += VP) {
+    f32x16 acc[VP];
 #pragma unroll
-  for (int v = 0; v < H::VTW; ++v) {
-    const int col = (wave * H::VTW + v) * 32 + r;
-    const float bb = bv[col], ww = wo[col];
+    for (int v = 0; v < VP; ++v) acc[v] = f32x16{};
+    constexpr int D = 2;  // weight ring depth
+    bf16x8 ring[D][VP];
+    const bf16x8 *wv = wf + (size_t)(1 + wave * H::VTW + v0) * H::KS * 64 + lane;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) part[i] += fmaxf(acc[v][i] + bb, 0.f) * ww;
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+      for (int v = 0; v < VP; ++v) ring[d][v] = wv[((size_t)v * H::KS + d) * 64];
+    bf16x8 avn = feat(0, FF);
+    for (int s0 = 0; s0 < H::KS; s0 += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int s = s0 + d;
+        if (s >= H::KS) break;
+        const bf16x8 av = avn;
+        if (s + 1 < H::KS) avn = feat(s + 1, FF);
+        bf16x8 wcur[VP];
+#pragma unroll
+        for (int v = 0; v < VP; ++v) {
+          wcur[v] = ring[d][v];
+          if (s + D < H::KS) ring[d][v] = wv[((size_t)v * H::KS + s + D) * 64];
+        }
+#pragma unroll
+        for (int v = 0; v < VP; ++v) acc[v] = Ty<E>::mfma(av, wcur[v], acc[v]);
+      }
+    }
+    // value: relu(acc + bv[col]) * wo[col], summed over the hidden units (cols); as k_heads
+#pragma unroll
+    for (int v = 0; v < VP; ++v) {
+      const int col = (wave * H::VTW + v0 + v) * 32 + r;
+      const float bb = bv[col], ww = wo[col];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) part[i] += fmaxf(acc[v][i] + bb, 0.f) * ww;
+    }
   }
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -1513,6 +1522,12 @@ static bool c256_board3() {
   return v != 0;
 }
 
+// C = 256 linear heads: the two-pass co-resident k_heads_co unless SPMCTS_HEADS_C256=lds (read per call)
+static bool heads_co256() {
+  const char *e = getenv("SPMCTS_HEADS_C256");
+  return !(e && strcmp(e, "lds") == 0);
+}
+
 // the instantiated tile sets of the device-count path, per board shape, channels and element type
 template <class E>
 static int forward_dev(int32_t width, int32_t height, int32_t channels, int32_t n_blocks, const void *planes_dev,
@@ -1684,10 +1699,11 @@ static int tower_heads(int32_t width, int32_t height, int32_t channels, int32_t 
   const int co = (he && strcmp(he, "lds") == 0) ? 0 : 1;
 #define HEADS(FF, CELLS, A)                                                                                   \
   do {                                                                                                        \
-  if (co && FF == 32) /* FF = 64 (C = 256) would spill at 96 registers; no room beside that trunk anyway */ \
-    hipLaunchKernelGGL((k_heads_co<FF, CELLS, A, E>), dim3((batch + 31) / 32), dim3(256), 0, s,               \
-                       (const uint16_t *)features_dev, batch, count_dev, (const bf16x8 *)head_w_dev, head_b_dev,\
-                       probs_dev, values_dev);                                                                \
+  /* C = 256 (FF = 64): two value passes of 2 tiles in 96 registers, beside the C = 256 trunk */          \
+  if (co && (FF == 32 || heads_co256()))                                                                     \
+    hipLaunchKernelGGL((k_heads_co<FF, CELLS, A, E, 5, FF == 64 ? 2 : HeadsCfg<FF, CELLS, A>::VTW>),          \
+                       dim3((batch + 31) / 32), dim3(256), 0, s, (const uint16_t *)features_dev, batch,       \
+                       count_dev, (const bf16x8 *)head_w_dev, head_b_dev, probs_dev, values_dev);             \
   else                                                                                                        \
     hipLaunchKernelGGL((k_heads<FF, CELLS, A, E>), dim3((batch + HeadsCfg<FF, CELLS, A>::BOARDS - 1) /        \
                                                      HeadsCfg<FF, CELLS, A>::BOARDS), dim3(256), 0, s,         \

@@ -36,12 +36,20 @@ def env_rank():
     return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("LOCAL_RANK", 0))
 
 
+def single_rank_group():
+    """SPMCTS_DIST_SINGLE=1: a process group even at world size 1, with every collective of the
+    multi-GPU path issued (rehearsal of the RCCL path on a 1-GPU box, where RCCL refuses two ranks
+    on one device)."""
+    return os.environ.get("SPMCTS_DIST_SINGLE", "0") == "1"
+
+
 def init_from_env(backend=None):
-    """Initialise torch.distributed from torchrun's environment (no-op for world size 1)."""
+    """Initialise torch.distributed from torchrun's environment (no-op for world size 1 unless
+    SPMCTS_DIST_SINGLE=1)."""
     rank, world, local = env_rank()
     if torch.cuda.is_available() and torch.cuda.device_count() > 0:
         local = local % torch.cuda.device_count()  # (rehearsals: several ranks on a 1-GPU box)
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or single_rank_group()) and not dist.is_initialized():
         if backend is None:
             backend = os.environ.get("SPMCTS_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -66,7 +74,7 @@ def local_device():
 
 
 def is_distributed():
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    return dist.is_available() and dist.is_initialized() and (dist.get_world_size() > 1 or single_rank_group())
 
 
 def _comm_device():

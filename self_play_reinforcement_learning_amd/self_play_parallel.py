@@ -92,7 +92,7 @@ class SelfPlayScheduler:
                  save_dir="saves", epoch_length=500, initial_games=64, lr=0.001, stagger=False, evaluation_games=100,
                  evaluation_network=None, stagger_mem_step=5000, deduplicate=False, update_delay=0.01,
                  self_play=None, n_games=None, device=None, seed=0, updates_per_ply=4, lanes=None, exchange_every=8,
-                 gpus=None, start_time=None, overlap_training=True):
+                 gpus=None, start_time=None, overlap_training=True, train_autocast=True):
         # constructor arguments, for rank processes started by this scheduler (_run_ranks)
         self._init_kwargs = {k: v for k, v in locals().items() if k not in ("self", "__class__")}
         self.policy_container = policy_container
@@ -116,6 +116,9 @@ class SelfPlayScheduler:
         self.updates_per_ply = updates_per_ply
         # the trainer's SGD steps on a HIP stream of their own, beside the arena's plies (_Trainer)
         self.overlap_training = overlap_training
+        # the UpdateWorker's update_from_memory runs under torch.cuda.amp.autocast() (fp16 on CUDA, no
+        # GradScaler; updateworker.py:148); False trains in fp32
+        self.train_autocast = train_autocast
         self.exchange_every = exchange_every  # plies per episode-batch exchange round (distributed.MoveExchange)
         # >1: LanedEngine (arenas on separate HIP streams, each a complete arena); None = 2 lanes for
         # arenas of >= 1,024 games, where the overlap pays (bench.py), else one arena
@@ -197,7 +200,7 @@ class SelfPlayScheduler:
         self.trainer = _Trainer(self.network, optim, memory_size=kw.get("memory_size", 200000),
                                 batch_size=kw.get("batch_size", 64), min_memory=kw.get("min_memory", 20000),
                                 q_average=kw.get("q_average", True), device=self.device, W=self.W, H=self.H,
-                                A=self.A, overlap=self.overlap_training)
+                                A=self.A, overlap=self.overlap_training, autocast=self.train_autocast)
         if resume_model:
             self._load_latest(prev_run=True)
         return self.trainer, None, None
@@ -483,7 +486,7 @@ class _Trainer:
     rows are overwritten and before the weights are read (checkpoint, weight refresh)."""
 
     def __init__(self, network, optim, memory_size, batch_size, min_memory, q_average, device, W=7, H=6, A=7,
-                 train_mode=True, overlap=True):
+                 train_mode=True, overlap=True, autocast=False):
         from .replay import DeviceReplay
 
         dev = torch.device(device) if device is not None else torch.device("cpu")
@@ -498,6 +501,10 @@ class _Trainer:
         self.q_average = q_average
         self.device = device
         self.train_mode = train_mode  # the UpdateWorker trains in train mode (updateworker.py:63)
+        # forward, loss and backward under fp16 autocast as the UpdateWorker (updateworker.py:147-149:
+        # `with autocast(): self.policy.update_from_memory()`, no GradScaler); only on a CUDA device,
+        # where the reference's autocast is active (it is a no-op on CPU)
+        self.autocast = bool(autocast) and dev.type == "cuda"
         self.scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optim, "max", patience=15, factor=0.5,
                                                                     min_lr=0.00001, cooldown=5)
 
@@ -526,10 +533,11 @@ class _Trainer:
 
     def _train_step(self, s, z, pi, q):
         self.network.train(self.train_mode)
-        loss = az_loss(self.network, s, z, pi, q, self.q_average)
-        self.optim.zero_grad()
-        loss.backward()
-        self.optim.step()
+        with torch.autocast("cuda", dtype=torch.float16, enabled=self.autocast):
+            loss = az_loss(self.network, s, z, pi, q, self.q_average)
+            self.optim.zero_grad()
+            loss.backward()
+            self.optim.step()
         self.network.eval()
         return loss.detach()
 

@@ -339,9 +339,11 @@ def test_spawn_ranks(tmp_path):
 
 
 def _exchange_worker(rank, world, port, q):
+    # SPMCTS_DIST_SINGLE: world size 1 runs the same collectives (the 1-GPU RCCL rehearsal's mode)
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
-                      SPMCTS_DIST_INIT="file://" + port)
+                      SPMCTS_DIST_INIT="file://" + port, SPMCTS_DIST_SINGLE="1")
     D.init_from_env(backend="gloo")
+    assert D.is_distributed()
     got = []
     ex = D.MoveExchange(42, 7, sink=lambda m: got.append({k: v.clone() for k, v in m.items()}), every=3)
     out = []
@@ -353,11 +355,12 @@ def _exchange_worker(rank, world, port, q):
     torch.distributed.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [1, 2, 4])
 def test_move_exchange_rounds_gloo(world):
     """Rounds every 3 plies (+ one forced): None between rounds; at a round every rank sees the
     same (all-done, summed stats); rank 0 receives exactly the rows staged since the previous round,
-    rank by rank, bit-exact after the device pack/unpack; the other ranks' sinks are never called."""
+    rank by rank, bit-exact after the device pack/unpack; the other ranks' sinks are never called.
+    World size 1 runs under SPMCTS_DIST_SINGLE=1 (a process group and every collective of one rank)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

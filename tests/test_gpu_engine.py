@@ -6,6 +6,8 @@ z in {-1, 0, 1} with the two trees of a game holding opposite results, the
 device counters balance (every simulation either reached the network or a
 terminal leaf), and no device error flag is raised.
 """
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -178,6 +180,35 @@ def test_trainer_steps_overlap_without_host_sync(tmp_path):
         out.append({k: v.clone() for k, v in net.state_dict().items()})
     for k in out[0]:  # same steps in the same order (backward kernels may differ in reduction order)
         torch.testing.assert_close(out[0][k], out[1][k], rtol=1e-4, atol=1e-6, msg=k)
+
+
+def test_trainer_autocast_matches_fp32_steps():
+    """_Trainer(autocast=True) runs the update under fp16 autocast as the reference's UpdateWorker
+    (updateworker.py:147-149, no GradScaler): the losses stay finite and within fp16 rounding of the
+    same steps in fp32, and the scheduler turns it on by default (train_autocast=True)."""
+    from self_play_reinforcement_learning_amd.modules import ResidualTower
+    from self_play_reinforcement_learning_amd.self_play_parallel import SelfPlayScheduler, _Trainer
+    import inspect
+
+    assert inspect.signature(SelfPlayScheduler).parameters["train_autocast"].default is True
+    g = torch.Generator().manual_seed(3)
+    rows = dict(state=torch.randint(-1, 2, (256, 42), dtype=torch.int8, generator=g),
+                tree_probs=torch.softmax(torch.randn(256, 7, generator=g), 1),
+                q=torch.rand(256, dtype=torch.float64, generator=g) - 0.5,
+                z=torch.randint(-1, 2, (256,), generator=g).float())
+    losses = {}
+    for ac in (False, True):
+        torch.manual_seed(0)
+        net = ResidualTower(7, 6, 7, num_blocks=2, filter_factor=16).cuda()
+        tr = _Trainer(net, torch.optim.SGD(net.parameters(), lr=0.01, momentum=0.9), memory_size=1000, batch_size=64,
+                      min_memory=0, q_average=True, device="cuda", overlap=False, autocast=ac)
+        assert tr.autocast is ac
+        tr.memory.add_moves(rows)
+        torch.manual_seed(5)
+        losses[ac] = [tr.step() for _ in range(6)]
+    assert all(math.isfinite(x) for x in losses[True])
+    for a, b in zip(losses[False], losses[True]):
+        assert abs(a - b) < 2e-2 * max(1.0, abs(a)), (losses[False], losses[True])
 
 
 @pytest.mark.parametrize("lanes", [1, 2])

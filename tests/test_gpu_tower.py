@@ -147,20 +147,24 @@ def test_zero_and_maximum_rows():
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("game,n", [("connect4", 1), ("connect4", 31), ("connect4", 33), ("connect4", 1000),
-                                    ("connect4", 4096), ("tictactoe", 77)])
-def test_coresident_heads_match_lds_heads(game, n, dtype, monkeypatch):
+@pytest.mark.parametrize("game,n,ff", [("connect4", 1, 32), ("connect4", 31, 32), ("connect4", 33, 32),
+                                       ("connect4", 1000, 32), ("connect4", 4096, 32), ("tictactoe", 77, 32),
+                                       ("connect4", 33, 64), ("connect4", 1000, 64), ("tictactoe", 77, 64)])
+def test_coresident_heads_match_lds_heads(game, n, ff, dtype, monkeypatch):
     """k_heads_co (features read from global memory, 32 boards per workgroup, 96 registers: fits beside
-    a trunk workgroup) gives the LDS-staged k_heads' results bit for bit: same per-wave k order, same
-    fixed-order cross-wave sums; ragged tails (n % 32) read only live boards."""
+    a trunk workgroup; C = 256: two value passes in 72 registers) gives the LDS-staged k_heads' results
+    bit for bit: same per-wave k order, same fixed-order cross-wave sums; ragged tails (n % 32) read
+    only live boards."""
     W, H, A = (7, 6, 7) if game == "connect4" else (3, 3, 9)
-    net = _net(W, H, A, 2, 32)
+    net = _net(W, H, A, 2, ff)
     x = _planes(W, H, n, seed=11).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     hip = HipTowerEvaluator(net, dtype=dtype)
     monkeypatch.setenv("SPMCTS_HEADS", "lds")
+    monkeypatch.setenv("SPMCTS_HEADS_C256", "lds")
     p0, v0 = hip(x)
     torch.cuda.synchronize()
     monkeypatch.delenv("SPMCTS_HEADS")
+    monkeypatch.delenv("SPMCTS_HEADS_C256")
     p1, v1 = hip(x)
     torch.cuda.synchronize()
     assert torch.equal(p0, p1) and torch.equal(v0, v1)
