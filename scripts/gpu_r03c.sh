@@ -13,6 +13,7 @@ tail -1 $O/smoke.log
 fi
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
 python -c "import json; d=json.loads([l for l in open('$O/bench.json') if l.startswith('{')][0]); print('bench', round(d['value']), round(d['roofline']['frac'],4), d['cpu_baseline']['value'])"
+[ "${1:-}" = SKIPC3 ] && exit 0
 for rep in 1 2; do
   for h in co lds; do
     SPMCTS_HEADS_C256=$h timeout -k 10 400 python3 -u bench.py --games 16384 --sims 800 --filter-factor 64 --warmup 3 \

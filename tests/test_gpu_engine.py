@@ -184,11 +184,14 @@ def test_trainer_steps_overlap_without_host_sync(tmp_path):
 
 def test_trainer_autocast_matches_fp32_steps():
     """_Trainer(autocast=True) runs the update under fp16 autocast as the reference's UpdateWorker
-    (updateworker.py:147-149, no GradScaler): the losses stay finite and within fp16 rounding of the
-    same steps in fp32, and the scheduler turns it on by default (train_autocast=True)."""
+    (updateworker.py:147-149, no GradScaler), and the scheduler turns it on by default
+    (train_autocast=True).  On one batch and the same starting weights (eval-mode dropout): the loss is
+    within fp16 rounding of the fp32 loss, and the SGD update points the same way (cosine of the
+    weight deltas)."""
+    import inspect
+
     from self_play_reinforcement_learning_amd.modules import ResidualTower
     from self_play_reinforcement_learning_amd.self_play_parallel import SelfPlayScheduler, _Trainer
-    import inspect
 
     assert inspect.signature(SelfPlayScheduler).parameters["train_autocast"].default is True
     g = torch.Generator().manual_seed(3)
@@ -196,19 +199,23 @@ def test_trainer_autocast_matches_fp32_steps():
                 tree_probs=torch.softmax(torch.randn(256, 7, generator=g), 1),
                 q=torch.rand(256, dtype=torch.float64, generator=g) - 0.5,
                 z=torch.randint(-1, 2, (256,), generator=g).float())
-    losses = {}
+    loss, delta, batch = {}, {}, None
     for ac in (False, True):
         torch.manual_seed(0)
         net = ResidualTower(7, 6, 7, num_blocks=2, filter_factor=16).cuda()
+        w0 = torch.cat([p.detach().reshape(-1).clone() for p in net.parameters()])
         tr = _Trainer(net, torch.optim.SGD(net.parameters(), lr=0.01, momentum=0.9), memory_size=1000, batch_size=64,
-                      min_memory=0, q_average=True, device="cuda", overlap=False, autocast=ac)
+                      min_memory=0, q_average=True, device="cuda", overlap=False, autocast=ac,
+                      train_mode=False)  # no dropout masks (their RNG differs between the dtypes)
         assert tr.autocast is ac
         tr.memory.add_moves(rows)
-        torch.manual_seed(5)
-        losses[ac] = [tr.step() for _ in range(6)]
-    assert all(math.isfinite(x) for x in losses[True])
-    for a, b in zip(losses[False], losses[True]):
-        assert abs(a - b) < 2e-2 * max(1.0, abs(a)), (losses[False], losses[True])
+        if batch is None:
+            batch = tr.memory.sample_batch(64)
+        loss[ac] = tr.train_batch(*batch)
+        delta[ac] = torch.cat([p.detach().reshape(-1) for p in net.parameters()]) - w0
+    assert math.isfinite(loss[True]) and abs(loss[True] - loss[False]) < 5e-3 * abs(loss[False]), loss
+    cos = torch.nn.functional.cosine_similarity(delta[True].double(), delta[False].double(), dim=0).item()
+    assert cos > 0.99, cos
 
 
 @pytest.mark.parametrize("lanes", [1, 2])
