@@ -139,7 +139,8 @@ struct Cfg : Ty<E_> {
   static constexpr int TAB = EDGE ? 9 * ROWS * 2 : 0;
   // ONEBUF (tower_wide.h): one activation buffer, convs in place between two barriers
   static constexpr bool ONEBUF = ONEBUF_;
-  static constexpr int LDS = (ONEBUF ? 1 : 2) * BUF + TAB;
+  // ONEBUF also stages each conv's bias (C floats) in LDS
+  static constexpr int LDS = (ONEBUF ? 1 : 2) * BUF + TAB + (ONEBUF ? C * 4 : 0);
   static constexpr int HEAD = C / 2;  // policy filter_factor | value filter_factor channels (filter_factor = C/4)
   static constexpr int HCT = HEAD / 32;  // head channel tiles
   static_assert(MT >= 1 && NT >= 1 && MT * NT <= (ONEBUF_ ? 16 : 8), "tile plan: at most 8 (one buffer: 16) accumulator tiles per wave");
@@ -1542,7 +1543,7 @@ static int forward_dev(int32_t width, int32_t height, int32_t channels, int32_t 
     using K3 = Cfg<256, 128, 7, 6, 4, 4, 0, 4, 1, false, false, E>;
     if (c256_board3())
       return launch_dyn<K3, K3, K3>(planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, pack, s);
-    return launch_dyn<Cfg<256, 256, 7, 6, 4, 4, 0, 4, 1, true, true, E, true>, K3, K3>(
+    return launch_dyn<Cfg<256, 256, 7, 6, 4, 4, 0, 2, 1, true, true, E, true>, K3, K3>(
         planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, pack, s);
   }
   if (width == 3 && height == 3 && channels == 128)
@@ -1630,7 +1631,7 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
     if (width == 7 && height == 6 && channels == 256) {
       using K3 = Cfg<256, 128, 7, 6, 4, 4, 0, 4, 1, false, false, E>;
       if (c256_board3()) return launch<K3>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-      return launch_split<Cfg<256, 256, 7, 6, 4, 4, 0, 4, 1, true, true, E, true>, K3, K3>(pl, batch, n_blocks,
+      return launch_split<Cfg<256, 256, 7, 6, 4, 4, 0, 2, 1, true, true, E, true>, K3, K3>(pl, batch, n_blocks,
                                                                                          weights_dev, bias_dev, ft, s);
     }
     if (width == 3 && height == 3 && channels == 128)
@@ -1677,7 +1678,7 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
   if (width == 7 && height == 6 && channels == 256) {  // as the device-count path
     using K3 = Cfg<256, 128, 7, 6, 4>;
     if (c256_board3()) return launch<K3>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-    return launch_split<Cfg<256, 256, 7, 6, 4, 4, 0, 4, 1, true, true, __bf16, true>, K3, K3>(pl, batch, n_blocks,
+    return launch_split<Cfg<256, 256, 7, 6, 4, 4, 0, 2, 1, true, true, __bf16, true>, K3, K3>(pl, batch, n_blocks,
                                                                                           weights_dev, bias_dev, ft, s);
   }
   if (width == 3 && height == 3 && channels == 128)

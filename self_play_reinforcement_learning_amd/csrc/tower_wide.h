@@ -43,21 +43,26 @@ template <class K, bool RESID, bool SAVE>
 __device__ __forceinline__ void epilogue(char *X, const f32x16 (&acc)[K::MT][K::NT], const float4 (&bv)[K::MT][4],
                                          uint4 *scr, int wave, int lane) {
   const int r = lane & 31, h = lane >> 5;
+  // residual reads in half batches of HT cell tiles (32 registers in flight instead of 64: the
+  // epilogue sits beside 256 accumulator AGPRs, and the full batch spilled)
+  constexpr int HT = K::NT / 2;
 #pragma unroll
-  for (int m = 0; m < K::MT; ++m) {
+  for (int mh = 0; mh < 2 * K::MT; ++mh) {
+    const int m = mh >> 1, t0 = (mh & 1) * HT;
     const int ct = wave * K::MT + m;  // CG = WAVES: wave w owns channel tiles [w*MT, (w+1)*MT)
-    uint4 res[RESID ? K::NT : 1][2];
+    uint4 res[RESID ? HT : 1][2];
     if constexpr (RESID) {
 #pragma unroll
-      for (int t = 0; t < K::NT; ++t) {
+      for (int i = 0; i < HT; ++i) {
         // nontemporal (nt): served from L2, never from a vector-L1 line an earlier read left behind
-        const u32x4 *p = (const u32x4 *)Scr<K>::at(scr, wave, m, t, lane);
-        res[t][0] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(p));
-        res[t][1] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(p + 1));
+        const u32x4 *p = (const u32x4 *)Scr<K>::at(scr, wave, m, t0 + i, lane);
+        res[i][0] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(p));
+        res[i][1] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(p + 1));
       }
     }
 #pragma unroll
-    for (int t = 0; t < K::NT; ++t) {
+    for (int i = 0; i < HT; ++i) {
+      const int t = t0 + i;
       char *p = X + (t * 32 + r) * K::RS + phys_off(ct, h, 0);
       uint32_t o[8];
 #pragma unroll
@@ -65,8 +70,8 @@ __device__ __forceinline__ void epilogue(char *X, const f32x16 (&acc)[K::MT][K::
         float v0 = acc[m][t][4 * g + 0] + bv[m][g].x, v1 = acc[m][t][4 * g + 1] + bv[m][g].y;
         float v2 = acc[m][t][4 * g + 2] + bv[m][g].z, v3 = acc[m][t][4 * g + 3] + bv[m][g].w;
         if constexpr (RESID) {
-          const f32x2 x0 = K::unpk(((const uint32_t *)&res[t][g >> 1])[2 * (g & 1)]);
-          const f32x2 x1 = K::unpk(((const uint32_t *)&res[t][g >> 1])[2 * (g & 1) + 1]);
+          const f32x2 x0 = K::unpk(((const uint32_t *)&res[i][g >> 1])[2 * (g & 1)]);
+          const f32x2 x1 = K::unpk(((const uint32_t *)&res[i][g >> 1])[2 * (g & 1) + 1]);
           v0 += x0[0];
           v1 += x0[1];
           v2 += x1[0];
@@ -100,11 +105,14 @@ __device__ __forceinline__ void load_bias(float4 (&bv)[K::MT][4], const float *b
 template <class K, int KK, int DEPTH, bool RESID, bool SAVE>
 __device__ __forceinline__ void conv(char *X, const Nbr<K> &nb, bf16x8 (&a)[DEPTH][K::MT], const float *bias, int wave,
                                      int lane, const WBuf &wb, uint32_t wl_off, uint32_t wn_off, int wn_steps,
-                                     uint4 *scr) {
+                                     uint4 *scr, float *sbias) {
   using Xl = XLive<K, 0>;
+  static_assert(K::C == K::THREADS, "one bias value per thread");
   const int hoff = 16 * (lane >> 5);
-  float4 bv[K::MT][4];  // the epilogue's bias, fetched now (its latency hides under the k-loop)
-  load_bias<K>(bv, bias, wave, lane);
+  // the epilogue's bias: one value per thread fetched now (its latency hides under the k-loop), staged
+  // in LDS at the end of the k-loop (1 register through the k-loop instead of the 32 of float4 bv[2][4];
+  // the previous layer's epilogue finished reading the staging area at its closing barrier)
+  const float bmine = bias[threadIdx.x];
   constexpr uint32_t ZP = Xl::ZPRE_T, LV0 = Xl::lt(0);
   f32x16 acc[K::MT][K::NT];
 #pragma unroll
@@ -123,7 +131,10 @@ __device__ __forceinline__ void conv(char *X, const Nbr<K> &nb, bf16x8 (&a)[DEPT
 #define TAPW(T) conv_tap_x<K, KK, DEPTH, 0, T>(X, nb, acc, bc, bn, off_cur, off_nxt, a, hoff, wb, wl_off, wn_off, wn_steps)
   TAPW(0); TAPW(1); TAPW(2); TAPW(3); TAPW(4); TAPW(5); TAPW(6); TAPW(7); TAPW(8);
 #undef TAPW
+  sbias[threadIdx.x] = bmine;
   __syncthreads();  // every wave has read the layer input: outputs may overwrite it
+  float4 bv[K::MT][4];
+  load_bias<K>(bv, sbias, wave, lane);
   epilogue<K, RESID, SAVE>(X, acc, bv, scr, wave, lane);
 }
 
@@ -180,6 +191,7 @@ __device__ __forceinline__ void tile(char *smem, const __bf16 *planes, int batch
   nb.init(lane & 31, 0);
   for (int i = tid; i < K::NZ * K::RS / 4; i += K::THREADS) ((uint32_t *)(X + K::ZROW * K::RS))[i] = 0u;
   uint16_t *tab = (uint16_t *)(smem + K::BUF);
+  float *sbias = (float *)(smem + K::BUF + K::TAB);  // the current conv's bias (K::C floats)
 #pragma unroll
   for (int j = 0; j < (9 * K::ROWS + K::THREADS - 1) / K::THREADS; ++j)
     if (9 * K::ROWS % K::THREADS == 0 || tid + j * K::THREADS < 9 * K::ROWS)
@@ -222,9 +234,9 @@ __device__ __forceinline__ void tile(char *smem, const __bf16 *planes, int batch
     const uint32_t wn_off = (kRingAlways && L + 1 == n_convs) ? wl_off : wl_off + (uint32_t)(LAYER * 16u);
     const int wn_steps = L + 1 < n_convs ? LSTEPS : 0;
     if ((L & 1) == 0)
-      conv<K, KK, DEPTH, false, false>(X, nb, ring, b, wave, lane, wb, wl_off, wn_off, wn_steps, scr);
+      conv<K, KK, DEPTH, false, false>(X, nb, ring, b, wave, lane, wb, wl_off, wn_off, wn_steps, scr, sbias);
     else
-      conv<K, KK, DEPTH, true, true>(X, nb, ring, b, wave, lane, wb, wl_off, wn_off, wn_steps, scr);
+      conv<K, KK, DEPTH, true, true>(X, nb, ring, b, wave, lane, wb, wl_off, wn_off, wn_steps, scr, sbias);
     b += K::C;
   }
   head_layer<K>(X, wblk + (size_t)n_convs * LAYER, b, out, board0, batch, wave, lane);
