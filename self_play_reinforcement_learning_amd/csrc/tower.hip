@@ -1512,13 +1512,14 @@ static int launch_dyn(const void *planes, const int32_t *count, int max_batch, i
 }  // namespace tower
 
 namespace tower {
-// The C = 256 trunk runs on 3-board two-buffer tiles unless SPMCTS_TOWER_C256=6 selects the 6-board
-// one-buffer tiles (tower_wide.h: bit-identical outputs, measured no faster).  Read once.
+// The C = 256 trunk runs on 6-board one-buffer edge tiles (tower_wide.h; bit-identical outputs, 3-4 %
+// faster than the 3-board two-buffer tiles since its bias moved to LDS) unless
+// SPMCTS_TOWER_C256=3 selects the 3-board tiles.  Read once.
 static bool c256_board3() {
   static int v = -1;
   if (v < 0) {
     const char *e = getenv("SPMCTS_TOWER_C256");
-    v = !(e && atoi(e) == 6);
+    v = e && atoi(e) == 3;
   }
   return v != 0;
 }
@@ -1539,7 +1540,7 @@ static int forward_dev(int32_t width, int32_t height, int32_t channels, int32_t 
                       Cfg<128, 128, 7, 6, 2, 4, 0, 4, 1, false, false, E>>(planes_dev, count_dev, max_batch, n_blocks,
                                                                           weights_dev, bias_dev, features_dev, pack, s);
   if (width == 7 && height == 6 && channels == 256) {
-    // 3-board two-buffer tiles; SPMCTS_TOWER_C256=6: 6-board one-buffer edge tiles (tower_wide.h), 3-board tails
+    // 6-board one-buffer edge tiles (tower_wide.h) with 3-board tails; SPMCTS_TOWER_C256=3: 3-board two-buffer tiles
     using K3 = Cfg<256, 128, 7, 6, 4, 4, 0, 4, 1, false, false, E>;
     if (c256_board3())
       return launch_dyn<K3, K3, K3>(planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, pack, s);
@@ -1678,6 +1679,9 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
   if (width == 7 && height == 6 && channels == 256) {  // as the device-count path
     using K3 = Cfg<256, 128, 7, 6, 4>;
     if (c256_board3()) return launch<K3>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+    if (cg == 254)  // timing alternative: the one-buffer trunk with a 4-deep weight ring (default 2)
+      return launch_split<Cfg<256, 256, 7, 6, 4, 4, 0, 4, 1, true, true, __bf16, true>, K3, K3>(pl, batch, n_blocks,
+                                                                                            weights_dev, bias_dev, ft, s);
     return launch_split<Cfg<256, 256, 7, 6, 4, 4, 0, 2, 1, true, true, __bf16, true>, K3, K3>(pl, batch, n_blocks,
                                                                                           weights_dev, bias_dev, ft, s);
   }
