@@ -224,6 +224,9 @@ def main():
                     help="node blocks per tree; below the worst case the arena recycles subtrees (k_compact)")
     ap.add_argument("--no-pack", action="store_true",
                     help="lanes > 1: keep round-aligned tower tiles (no SPMCTS_TOWER_PACK)")
+    ap.add_argument("--twin-no-dedup", type=int, default=0, metavar="PLIES",
+                    help="after the timed region, turn leaf dedup off and time PLIES more plies of the same games "
+                         "(every leaf its own row, as the reference): reported as no_dedup_twin")
     ap.add_argument("--progress", action="store_true",
                     help="one stderr line per untimed ply (long warm-ups, e.g. config 3 in steady state)")
     ap.add_argument("--dtype", choices=["bf16", "fp16"], default="bf16",
@@ -491,6 +494,32 @@ def main():
                                      f"games per GPU, policy ResNet-{4 * args.filter_factor}x{args.blocks} (seed 0) vs "
                                      f"opponent (seed 1), evaluate mode (temp/20, noise on), no Move records")
     out["cpu_baseline"] = cpu
+    if args.twin_no_dedup > 0 and getattr(eng, "leaf_dedup", False):
+        # the same arenas, right after the timed region: every leaf gets its own network row
+        for e in getattr(eng, "lanes", [eng]):
+            e.arena.set_leaf_dedup(False)
+            e.leaf_dedup = False
+        eng.leaf_dedup = False
+        eng.check()
+        t_c0 = eng.counters()
+        D.barrier()
+        torch.cuda.synchronize()
+        t_t0 = time.perf_counter()
+        for _ in range(args.twin_no_dedup):
+            one_step()
+        if D.is_distributed() and args.twin_no_dedup % args.exchange_every:
+            ex.end_ply(eng.stats_vector, force=True)
+        D.barrier()
+        torch.cuda.synchronize()
+        t_el = D.all_reduce_max(time.perf_counter() - t_t0)
+        t_c1 = eng.counters()
+        eng.check()
+        t_moves = int(D.all_reduce_stats([t_c1["moves"] - t_c0["moves"]])[0])
+        out["no_dedup_twin"] = {
+            "plies": args.twin_no_dedup, "value": t_moves / t_el, "ms_per_step": t_el / args.twin_no_dedup * 1e3,
+            "rows_per_leaf": (t_c1["nn_rows"] - t_c0["nn_rows"]) / max(1, t_c1["nn_leaves"] - t_c0["nn_leaves"]),
+            "note": "the plies right after the timed region, leaf dedup off (spmcts_set_leaf_dedup): every leaf "
+                    "evaluated in its own row, as the reference's InferenceWorker"}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if D.is_distributed():

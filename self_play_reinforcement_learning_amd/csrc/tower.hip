@@ -25,6 +25,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -1079,13 +1080,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const __bf16 *planes, const int32_t *count, int max_batch, int cus, int n_blocks, const bf16x8 *wpk,
     const float *bias, uint16_t *out, uint4 *scr) {
   static_assert(KF::THREADS == 256 && KM::THREADS == 256 && KH::THREADS == 256, "one block size");
-  static_assert(!KM::ONEBUF && !KH::ONEBUF, "residual scratch is sized for the full tiles only");
+  // residual scratch is sized per workgroup of the full tiles (scratch_bytes<KF>): a one-buffer tail tile
+  // must be the full tile itself
+  static_assert((!KM::ONEBUF || std::is_same<KM, KF>::value) && (!KH::ONEBUF || std::is_same<KH, KF>::value),
+                "one-buffer tail tiles must be the full tiles");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int n = min(*count, max_batch);  // never past the caller's buffers
   const int full_wgs = (n / KF::BOARDS) / cus * cus;
   const int n_full = full_wgs * KF::BOARDS;
   const int rem = n - n_full;
   const int b = blockIdx.x;
+  if constexpr (std::is_same<KM, KF>::value && std::is_same<KH, KF>::value) {
+    // one tile kind: one inlined copy of the tile body (whole rounds and the tail alike)
+    const int board0 = b < full_wgs ? b * KF::BOARDS : n_full + (b - full_wgs) * KF::BOARDS;
+    if (board0 < n) tower_tile<KF>(smem, planes, n, board0, n_blocks, wpk, bias, out, scr);
+    return;
+  }
   if (b < full_wgs) {
     tower_tile<KF>(smem, planes, n, b * KF::BOARDS, n_blocks, wpk, bias, out, scr);
     return;
@@ -1524,6 +1534,16 @@ static bool c256_board3() {
   return v != 0;
 }
 
+// packed C = 256 launches: one-buffer tail tiles unless SPMCTS_WIDE_TAILS=3.  Read once.
+static bool wide_tails3() {
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("SPMCTS_WIDE_TAILS");
+    v = e && atoi(e) == 3;
+  }
+  return v != 0;
+}
+
 // C = 256 linear heads: the two-pass co-resident k_heads_co unless SPMCTS_HEADS_C256=lds (read per call)
 static bool heads_co256() {
   const char *e = getenv("SPMCTS_HEADS_C256");
@@ -1542,10 +1562,14 @@ static int forward_dev(int32_t width, int32_t height, int32_t channels, int32_t 
   if (width == 7 && height == 6 && channels == 256) {
     // 6-board one-buffer edge tiles (tower_wide.h) with 3-board tails; SPMCTS_TOWER_C256=3: 3-board two-buffer tiles
     using K3 = Cfg<256, 128, 7, 6, 4, 4, 0, 4, 1, false, false, E>;
+    using KW = Cfg<256, 256, 7, 6, 4, 4, 0, 2, 1, true, true, E, true>;
     if (c256_board3())
       return launch_dyn<K3, K3, K3>(planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, pack, s);
-    return launch_dyn<Cfg<256, 256, 7, 6, 4, 4, 0, 2, 1, true, true, E, true>, K3, K3>(
-        planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, pack, s);
+    // packed launches (lanes beside each other) have a tail of < 6 boards: one 6-board tile takes it, and a
+    // kernel with the one-buffer code path only holds fewer registers (SPMCTS_WIDE_TAILS=3: 3-board tail code)
+    if (pack && !wide_tails3())
+      return launch_dyn<KW, KW, KW>(planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, pack, s);
+    return launch_dyn<KW, K3, K3>(planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, pack, s);
   }
   if (width == 3 && height == 3 && channels == 128)
     return launch_dyn<Cfg<128, 256, 3, 3, 2, 4, 0, 4, 1, false, false, E>, Cfg<128, 192, 3, 3, 2, 4, 0, 4, 1, false, false, E>,
