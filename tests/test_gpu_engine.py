@@ -602,3 +602,28 @@ def test_leaf_dedup_two_networks_exact():
     for k in ("sims", "moves", "nn_leaves", "terminal_leaves", "depth_sum", "games_finished", "results"):
         assert c0[k] == c1[k], k
     assert c1["nn_rows"] < c1["nn_leaves"]
+
+
+def test_bench_line_small_with_no_dedup_twin():
+    """bench.py end to end on a small workload (subprocess, as the driver runs it): one JSON line with
+    the contract keys, roofline and tree roofline, and the --twin-no-dedup plies (leaf dedup off on
+    the same arenas: one network row per leaf)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--games", "512", "--sims", "16", "--blocks", "2",
+           "--steps", "3", "--warmup", "2", "--no-cpu-baseline", "--twin-no-dedup", "2"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=root, check=True).stdout
+    line = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(line) == 1
+    d = json.loads(line[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "dtype", "data", "config", "roofline", "tree_roofline", "exchange"):
+        assert k in d, k
+    assert d["value"] > 0 and d["n_gpus"] == 1 and d["steps"] == 3 and d["exchange"]["backend"] is None
+    assert 0 < d["roofline"]["frac"] < 1 and d["config"]["leaf_dedup"] is True and d["nn"]["rows_per_leaf"] <= 1.0
+    tw = d["no_dedup_twin"]
+    assert tw["plies"] == 2 and tw["value"] > 0 and tw["rows_per_leaf"] == 1.0
