@@ -3,7 +3,8 @@
 
 BASELINE.json metric "self-play positions/sec (Connect4, 200 sims/move) at
 1/2/4/8 MI355X" on configs[1]: ResNet-128 (ResidualTower filter_factor=32,
-num_blocks=20, random init, torch.manual_seed(0)), bf16 leaf evaluation.
+num_blocks=20, random init, torch.manual_seed(0)), fp16 leaf evaluation (the reference's
+autocast inference dtype; --dtype bf16 for the bf16 trunk, reported as secondary_dtype by default).
 
 A *step* is one ply of every game slot of every rank: 200 PUCT simulations
 (select -> ResNet -> expand/backup) per game, then the move, Move records,
@@ -224,14 +225,17 @@ def main():
                     help="node blocks per tree; below the worst case the arena recycles subtrees (k_compact)")
     ap.add_argument("--no-pack", action="store_true",
                     help="lanes > 1: keep round-aligned tower tiles (no SPMCTS_TOWER_PACK)")
-    ap.add_argument("--twin-no-dedup", type=int, default=0, metavar="PLIES",
+    ap.add_argument("--twin-no-dedup", type=int, default=5, metavar="PLIES",
                     help="after the timed region, turn leaf dedup off and time PLIES more plies of the same games "
                          "(every leaf its own row, as the reference): reported as no_dedup_twin")
     ap.add_argument("--progress", action="store_true",
                     help="one stderr line per untimed ply (long warm-ups, e.g. config 3 in steady state)")
-    ap.add_argument("--dtype", choices=["bf16", "fp16"], default="bf16",
-                    help="element type of the fused trunk's weights / activations (fp32 accumulation); fp16 is the "
-                         "reference's own inference dtype (amp.autocast, inference_worker.py:117)")
+    ap.add_argument("--dtype", choices=["bf16", "fp16"], default="fp16",
+                    help="element type of the fused trunk's weights / activations (fp32 accumulation); fp16 (the "
+                         "default) is the reference's own inference dtype (amp.autocast, inference_worker.py:117)")
+    ap.add_argument("--secondary-plies", type=int, default=5, metavar="PLIES",
+                    help="after the timed region (and the no-dedup twin), time PLIES more plies of the same games "
+                         "with the other trunk dtype (bf16 <-> fp16): reported as secondary_dtype")
     ap.add_argument("--search-threads", type=int, default=4,
                     help="sims in flight per tree with virtual loss: the reference's thread_count search "
                          "(mcts.py:328-331), 4 in its headline self-play setup (InferenceProxy workers, "
@@ -294,7 +298,8 @@ def main():
 
     def one_step():
         eng.ply(on_moves=ex.stage if not (args.no_gather or arena_mode) else None)
-        ex.end_ply(eng.stats_vector)
+        # statistics are read (a host sync on the device counters) only for a real exchange round
+        ex.end_ply(eng.stats_vector if D.is_distributed() else None)
 
     tw = time.perf_counter()
     for i in range(args.warmup):
@@ -327,6 +332,9 @@ def main():
     c1 = eng.counters()
     eng.check()
     moves_local = c1["moves"] - c0["moves"]
+    # per-rank lines (an all_gather on every rank): stragglers and exchange cost show in a scaling record
+    per_rank = D.rank_report([moves_local / elapsed if elapsed else 0.0, elapsed, ex.rounds,
+                              ex.seconds / max(1, ex.rounds) * 1e3, ex.rows_gathered])
     tot = D.all_reduce_stats([moves_local, c1["sims"] - c0["sims"], c1["games_finished"] - c0["games_finished"]])
     moves_all, sims_all, games_all = (int(x) for x in tot)
 
@@ -468,6 +476,14 @@ def main():
             "nn_ms": nn_ms,
             "share_of_step": nn_ms / 1e3 / elapsed if elapsed else None,
         },
+        "ranks": {
+            "world_size": torch.distributed.get_world_size() if D.is_distributed() else 1,
+            "backend": torch.distributed.get_backend() if D.is_distributed() else None,
+            "positions_per_s_min": min(r[0] for r in per_rank),
+            "positions_per_s_max": max(r[0] for r in per_rank),
+            "per_rank": [{"rank": i, "positions_per_s": r[0], "timed_s": r[1], "exchange_rounds": int(r[2]),
+                          "exchange_ms_per_round": r[3], "rows_received": int(r[4])} for i, r in enumerate(per_rank)],
+        },
         "exchange": {"backend": torch.distributed.get_backend() if D.is_distributed() else None,
                      "every_plies": args.exchange_every, "rounds": ex.rounds, "rows_to_rank0": ex.rows_gathered,
                      "ms_per_round": ex.seconds / max(1, ex.rounds) * 1e3,
@@ -520,6 +536,37 @@ def main():
             "rows_per_leaf": (t_c1["nn_rows"] - t_c0["nn_rows"]) / max(1, t_c1["nn_leaves"] - t_c0["nn_leaves"]),
             "note": "the plies right after the timed region, leaf dedup off (spmcts_set_leaf_dedup): every leaf "
                     "evaluated in its own row, as the reference's InferenceWorker"}
+    if args.secondary_plies > 0 and not arena_mode:
+        # the same games with the trunk in the other element type (a secondary figure; `value` is the
+        # --dtype line): every lane's fused evaluator repacks its weights (HipTowerEvaluator.set_dtype)
+        other = {"bf16": "fp16", "fp16": "bf16"}[args.dtype]
+        evs = [e.evaluator for e in getattr(eng, "lanes", [eng])]
+        if all(hasattr(ev, "set_dtype") for ev in evs):
+            for ev in evs:
+                ev.set_dtype({"bf16": torch.bfloat16, "fp16": torch.float16}[other])
+            eng.refresh_network()
+            eng.check()
+            s_c0 = eng.counters()
+            D.barrier()
+            torch.cuda.synchronize()
+            s_t0 = time.perf_counter()
+            for _ in range(args.secondary_plies):
+                one_step()
+            if D.is_distributed() and args.secondary_plies % args.exchange_every:
+                ex.end_ply(eng.stats_vector, force=True)
+            D.barrier()
+            torch.cuda.synchronize()
+            s_el = D.all_reduce_max(time.perf_counter() - s_t0)
+            s_c1 = eng.counters()
+            eng.check()
+            s_moves = int(D.all_reduce_stats([s_c1["moves"] - s_c0["moves"]])[0])
+            out["secondary_dtype"] = {
+                "dtype": other, "plies": args.secondary_plies, "value": s_moves / s_el,
+                "ms_per_step": s_el / args.secondary_plies * 1e3,
+                "leaf_dedup": bool(getattr(eng, "leaf_dedup", False)),
+                "rows_per_leaf": (s_c1["nn_rows"] - s_c0["nn_rows"]) / max(1, s_c1["nn_leaves"] - s_c0["nn_leaves"]),
+                "note": f"the plies after the timed region{' and the no-dedup twin' if 'no_dedup_twin' in out else ''}, "
+                        f"the fused trunk and heads repacked in {other}"}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if D.is_distributed():

@@ -61,6 +61,13 @@ enum spmcts_player_kind {
   SPMCTS_PLAYER_LOOKAHEAD = 2 /* OneStepLookahead: win / block / random (:8-33)               */
 };
 
+/* return code of the tower entry points (spmcts_tower_forward*, spmcts_tower_heads*) and of
+ * spmcts_arena_create: an environment switch of the A/B library (SPMCTS_TOWER_CG, SPMCTS_TOWER_RING,
+ * SPMCTS_TOWER_C256, SPMCTS_WIDE_TAILS, SPMCTS_HEADS, SPMCTS_HEADS_C256, SPMCTS_TREE_BLOCK,
+ * SPMCTS_EXPAND_CO; `make ab` builds libspmcts_ab.so, which reads them) is set while the product
+ * library is loaded: refused instead of silently ignored */
+#define SPMCTS_ERR_AB_SWITCH (-5)
+
 /* device error flags (sticky) */
 #define SPMCTS_ERR_POOL 0x1u      /* a tree ran out of node blocks                 */
 #define SPMCTS_ERR_TAPE 0x2u      /* RNG tape exhausted                            */

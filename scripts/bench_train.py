@@ -19,7 +19,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def run(args, updates, overlap, autocast=True):
+def run(args, updates, overlap, autocast=True, graph=True):
     import torch
 
     from self_play_reinforcement_learning_amd import Connect4Env, MCTreeSearch, ModelContainer, SelfPlayScheduler
@@ -30,7 +30,7 @@ def run(args, updates, overlap, autocast=True):
     kw = dict(iterations=args.sims, env=Connect4Env, batch_size=64, memory_size=200000, min_memory=args.min_memory)
     sp = SelfPlayScheduler(ModelContainer(MCTreeSearch, policy_kwargs=kw), Connect4Env, network=net, save_dir=None,
                            n_games=args.games, updates_per_ply=updates, overlap_training=overlap, evaluation_games=0,
-                           train_autocast=autocast,
+                           train_autocast=autocast, train_graph=graph,
                            lr=0.001)
     sp.setup_player_workers()
     sp.setup_update_worker()
@@ -56,9 +56,41 @@ def run(args, updates, overlap, autocast=True):
     dt = time.perf_counter() - t0
     moves, steps = eng.counters()["moves"] - m0, tr.steps - s0
     loss = float(tr.last_loss) if tr.last_loss is not None else None
-    return dict(updates_per_ply=updates, trainer_stream=overlap, train_autocast=autocast, plies=args.plies, seconds=dt,
+    return dict(updates_per_ply=updates, trainer_stream=tr.stream is not None, train_autocast=autocast, train_graph=graph,
+                graph_captures=tr.graph_captures, plies=args.plies, seconds=dt,
                 positions_per_s=moves / dt, sgd_steps=steps, sgd_steps_per_s=steps / dt, fill_plies=fill_plies,
                 replay_rows=len(tr.memory), last_loss=loss)
+
+
+def trainer_only(args, graph, autocast=True, steps=40):
+    """ms per SGD step of the trainer alone (batch 64, ResNet-128x20, train mode), graphed or eager."""
+    import torch
+
+    from self_play_reinforcement_learning_amd.modules import ResidualTower
+    from self_play_reinforcement_learning_amd.self_play_parallel import _Trainer
+
+    torch.manual_seed(0)
+    net = ResidualTower(7, 6, 7, num_blocks=20, filter_factor=32).cuda()
+    tr = _Trainer(net, torch.optim.SGD(net.parameters(), lr=0.001, momentum=0.9, weight_decay=1e-4), memory_size=200000,
+                  batch_size=64, min_memory=0, q_average=True, device="cuda", overlap=True, autocast=autocast,
+                  graph=graph)
+    g = torch.Generator().manual_seed(0)
+    n = 20000
+    tr.memory.add_moves(dict(state=torch.randint(-1, 2, (n, 42), dtype=torch.int8, generator=g),
+                             tree_probs=torch.softmax(torch.randn(n, 7, generator=g), 1),
+                             q=torch.rand(n, dtype=torch.float64, generator=g), z=torch.randint(-1, 2, (n,), generator=g).float()))
+    for _ in range(6):
+        tr.step()
+    tr.sync()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.step()
+    tr.sync()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return dict(train_graph=graph, train_autocast=autocast, steps=steps, ms_per_sgd_step=dt / steps * 1e3,
+                graph_captures=tr.graph_captures, last_loss=float(tr.last_loss))
 
 
 def main():
@@ -71,9 +103,9 @@ def main():
     args = ap.parse_args()
     out = dict(workload=f"connect4 self-play + training, {args.sims} sims, {args.games} games, ResNet-128x20 (bf16 "
                         f"trunk for leaves, SGD batch 64 under fp16 autocast as updateworker.py:148, or fp32), K = 4, two lanes",
-               runs=[run(args, args.updates, True), run(args, args.updates, False),
-                     run(args, args.updates, True, autocast=False), run(args, args.updates, False, autocast=False),
-                     run(args, 0, True)])
+               trainer_only=[trainer_only(args, True), trainer_only(args, False), trainer_only(args, True, False)],
+               runs=[run(args, args.updates, True), run(args, args.updates, True, graph=False),
+                     run(args, args.updates, False), run(args, 0, True)])
     print(json.dumps(out), flush=True)
 
 

@@ -1,6 +1,6 @@
 """Bit-equality of a timing alternative (SPMCTS_TOWER_CG) with the default trunk: run once per code
 (the switch is read once per process) writing the host-path outputs, then compare the files.
-  python scripts/tower_code_equal.py dump OUT.npz [FILTER_FACTOR]   |   python scripts/tower_code_equal.py cmp A.npz B.npz"""
+  python scripts/tower_code_equal.py dump OUT.npz [FILTER_FACTOR [bf16|fp16]]   |   python scripts/tower_code_equal.py cmp A.npz B.npz"""
 import sys
 
 import os
@@ -10,7 +10,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def dump(out, ff=32):
+def dump(out, ff=32, dtype="bf16"):
     import torch
 
     from self_play_reinforcement_learning_amd.evaluator import HipTowerEvaluator
@@ -29,7 +29,7 @@ def dump(out, ff=32):
         b = np.random.default_rng(1).choice([-1, 0, 1], size=(4000, 7, 6), p=[0.3, 0.4, 0.3])
         x = planes_from_boards(torch.as_tensor(b), 7, 6).cuda()
         x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        ev = HipTowerEvaluator(net)
+        ev = HipTowerEvaluator(net, dtype={"bf16": torch.bfloat16, "fp16": torch.float16}[dtype])
         p, v = ev(x)
         res[f"p{blocks}"] = p.float().cpu().numpy()
         res[f"v{blocks}"] = v.float().cpu().numpy()
@@ -52,6 +52,6 @@ def cmp(a, b):
 
 if __name__ == "__main__":
     if sys.argv[1] == "dump":
-        dump(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 32)
+        dump(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 32, sys.argv[4] if len(sys.argv) > 4 else "bf16")
     else:
         sys.exit(cmp(sys.argv[2], sys.argv[3]))

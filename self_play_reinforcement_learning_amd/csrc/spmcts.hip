@@ -2153,13 +2153,24 @@ int spmcts_arena_create(const spmcts_config *cfg, int device, spmcts_arena **out
     delete h;
     return rc;
   }
+#ifndef SPMCTS_AB
+  for (const char *n : {"SPMCTS_TREE_BLOCK", "SPMCTS_EXPAND_CO"})
+    if (getenv(n)) {
+      delete h;
+      return fail(SPMCTS_ERR_AB_SWITCH, std::string(n) + " is a switch of the A/B library (make ab: libspmcts_ab.so)");
+    }
+#endif
   {
     // Threads per workgroup of the threaded tree kernels (SPMCTS_TREE_BLOCK): P = one tree per wave,
     // 64 = one wave of 64/P trees, 128..512 = 2..8 such waves.  A tree-kernel wave (~170 VGPRs) leaves no
     // room on its SIMD for a trunk wave (416 registers), so each tree workgroup keeps a whole CU away from
     // the other lane's trunk launch while it runs: fewer, fuller workgroups block fewer CUs.
-    const char *e = getenv("SPMCTS_TREE_BLOCK");
+#ifdef SPMCTS_AB
+    const char *e = getenv("SPMCTS_TREE_BLOCK");  // A/B library only (64 measured best)
     const int tb = e ? atoi(e) : 64;
+#else
+    const int tb = 64;
+#endif
     h->tree_block = (tb == h->P || (tb >= 64 && tb <= 512 && tb % 64 == 0)) ? tb : 64;
   }
   hipError_t e = hipSetDevice(device);
@@ -2281,9 +2292,11 @@ int spmcts_select_tree(spmcts_arena *h, spmcts_stream stream) {
     const int gpb = 64 / h->P;
     if (h->v.K > 1) {
       const int tb = h->tree_block, tpb = tb / h->P;
+#ifdef SPMCTS_AB
       if (tb > 64)
         DISPATCH(h, hipLaunchKernelGGL((k_select_vl<GG, 512>), dim3(nblk(n, tpb)), dim3(tb), 0, s, h->v, n));
       else
+#endif
         DISPATCH(h, hipLaunchKernelGGL(k_select_vl<GG>, dim3(nblk(n, tpb)), dim3(tb), 0, s, h->v, n));
     } else {
       DISPATCH(h, hipLaunchKernelGGL(k_select<GG>, dim3(nblk(n, gpb)), dim3(64), 0, s, h->v, n));
@@ -2313,7 +2326,8 @@ int spmcts_expand2(spmcts_arena *h, const float *probs0_dev, const float *values
   const int gpb = 64 / h->P;
   if (h->v.K > 1) {
     const int tb = h->tree_block, tpb = tb / h->P;
-    static int co = -1;
+#ifdef SPMCTS_AB
+    static int co = -1;  // A/B library only: the 96-register co-resident expand (measured slower)
     if (co < 0) {
       const char *e = getenv("SPMCTS_EXPAND_CO");
       co = e && atoi(e) ? 1 : 0;
@@ -2325,6 +2339,7 @@ int spmcts_expand2(spmcts_arena *h, const float *probs0_dev, const float *values
       DISPATCH(h, hipLaunchKernelGGL((k_expand_vl<GG, 512>), dim3(nblk(h->v.T, tpb)), dim3(tb), 0, (hipStream_t)stream,
                                      h->v, probs0_dev, values0_dev, probs1_dev, values1_dev));
     else
+#endif
       DISPATCH(h, hipLaunchKernelGGL(k_expand_vl<GG>, dim3(nblk(h->v.T, tpb)), dim3(tb), 0, (hipStream_t)stream, h->v,
                                      probs0_dev, values0_dev, probs1_dev, values1_dev));
   } else {

@@ -166,9 +166,13 @@ struct Cfg : Ty<E_> {
     return EDGE ? (kEdgeRow[row] >> 3) & 7 : XMAJ ? row / (BOARDS * H) : (row % CELLS) / H;
   }
   __host__ __device__ static constexpr int row_y(int row) { return EDGE ? kEdgeRow[row] & 7 : row % H; }
+  // does row `row` (< ROWS) hold a cell?  Board-major / column-major tiles: rows < VROWS; edge tiles: the
+  // rows tower_edge.h does not mark as padding (255), which may sit anywhere in the tile
+  __host__ __device__ static constexpr bool row_ok(int row) { return EDGE ? kEdgeRow[row] != 255 : row < VROWS; }
   // does any on-board row of cell tile T have an on-board neighbour for `tap`?
   __host__ __device__ static constexpr bool tile_tap_live(int T, int tap) {
-    for (int r = T * 32; r < T * 32 + 32 && r < VROWS; ++r) {
+    for (int r = T * 32; r < T * 32 + 32 && r < ROWS; ++r) {
+      if (!row_ok(r)) continue;
       const int nx = row_x(r) + tap / 3 - 1, ny = row_y(r) + tap % 3 - 1;
       if (nx >= 0 && nx < W && ny >= 0 && ny < H) return true;
     }
@@ -177,7 +181,8 @@ struct Cfg : Ty<E_> {
   __host__ __device__ static constexpr int row_cell(int row) { return row_x(row) * H + row_y(row); }
   // does any on-board row of 32-row cell tile T have an on-board neighbour column x + dx?
   __host__ __device__ static constexpr bool tile_dx_live(int T, int dx) {
-    for (int r = T * 32; r < T * 32 + 32 && r < VROWS; ++r) {
+    for (int r = T * 32; r < T * 32 + 32 && r < ROWS; ++r) {
+      if (!row_ok(r)) continue;
       const int nx = row_x(r) + dx;
       if (nx >= 0 && nx < W) return true;
     }
@@ -222,7 +227,7 @@ struct Nbr {
       base[t] = row * K::RS;
       rowi[t] = row;
       uint32_t m = 0;
-      if (row < K::VROWS) {
+      if (K::row_ok(row)) {
         const int x = K::row_x(row), y = K::row_y(row);
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
@@ -924,9 +929,9 @@ __device__ __forceinline__ void head_layer(const char *src, const bf16x8 *w, con
 #pragma unroll
   for (int t = 0; t < TPW; ++t) {
     const int row = (t0 + t) * 32 + r;
-    const int rr = row < K::VROWS ? row : 0;
+    const int rr = K::row_ok(row) ? row : 0;
     const int board = board0 + K::row_board(rr);
-    okr[t] = row < K::VROWS && board < batch;
+    okr[t] = K::row_ok(row) && board < batch;
     obase[t] = ((size_t)board * K::CELLS + K::row_cell(rr)) * K::HEAD;
   }
 #pragma unroll
@@ -982,7 +987,7 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
   for (int row = tid; row < K::ROWS; row += K::THREADS) {
     const int board = board0 + K::row_board(row);
     uint16_t *dst = (uint16_t *)(Y + row * K::RS);
-    const bool ok = row < K::VROWS && board < batch;
+    const bool ok = K::row_ok(row) && board < batch;
     const size_t src = ((size_t)board * K::CELLS + K::row_cell(row)) * 3;
 #pragma unroll
     for (int c = 0; c < 16; ++c) dst[c] = (ok && c < 3) ? K::from_bf16(planes[src + c]) : (uint16_t)0;
@@ -1052,7 +1057,9 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
   head_layer<K>(X, w, b, out, board0, batch, wave, lane);
 }
 
-#include "tower_ring.h"
+#ifdef SPMCTS_AB
+#include "tower_ring.h"  // the LDS weight-ring trunk (measured 3-6 % slower; A/B library only)
+#endif
 
 template <class K>
 __global__ __launch_bounds__(K::THREADS) __attribute__((amdgpu_waves_per_eu(K::WAVES / 4 * K::OCC, K::WAVES / 4 * K::OCC))) void k_tower(
@@ -1522,32 +1529,50 @@ static int launch_dyn(const void *planes, const int32_t *count, int max_batch, i
 }  // namespace tower
 
 namespace tower {
-// The C = 256 trunk runs on 6-board one-buffer edge tiles (tower_wide.h; bit-identical outputs, 3-4 %
-// faster than the 3-board two-buffer tiles since its bias moved to LDS) unless
-// SPMCTS_TOWER_C256=3 selects the 3-board tiles.  Read once.
-static bool c256_board3() {
-  static int v = -1;
-  if (v < 0) {
-    const char *e = getenv("SPMCTS_TOWER_C256");
-    v = e && atoi(e) == 3;
-  }
-  return v != 0;
+#ifdef SPMCTS_AB
+// A/B library (make ab: libspmcts_ab.so, -DSPMCTS_AB) only: switches that select measured-slower
+// alternates and timing ablations.  Read once.
+static bool env_is(const char *name, const char *val) {
+  const char *e = getenv(name);
+  return e && strcmp(e, val) == 0;
 }
-
-// packed C = 256 launches: one-buffer tail tiles unless SPMCTS_WIDE_TAILS=3.  Read once.
-static bool wide_tails3() {
-  static int v = -1;
-  if (v < 0) {
-    const char *e = getenv("SPMCTS_WIDE_TAILS");
-    v = e && atoi(e) == 3;
-  }
-  return v != 0;
+static bool c256_board3() {  // SPMCTS_TOWER_C256=3: the C = 256 trunk on 3-board two-buffer tiles
+  static const bool v = env_is("SPMCTS_TOWER_C256", "3");
+  return v;
 }
-
-// C = 256 linear heads: the two-pass co-resident k_heads_co unless SPMCTS_HEADS_C256=lds (read per call)
-static bool heads_co256() {
-  const char *e = getenv("SPMCTS_HEADS_C256");
-  return !(e && strcmp(e, "lds") == 0);
+static bool wide_tails3() {  // SPMCTS_WIDE_TAILS=3: packed C = 256 launches with 3-board tail code
+  static const bool v = env_is("SPMCTS_WIDE_TAILS", "3");
+  return v;
+}
+static bool heads_co256() {  // SPMCTS_HEADS_C256=lds: the LDS-staged C = 256 linear heads
+  static const bool v = !env_is("SPMCTS_HEADS_C256", "lds");
+  return v;
+}
+static bool heads_co() {  // SPMCTS_HEADS=lds: the LDS-staged linear heads
+  static const bool v = !env_is("SPMCTS_HEADS", "lds");
+  return v;
+}
+#else
+// The product library has exactly one kernel per (shape, dtype) and reads no switch; a switch of the
+// A/B library set in the environment is refused (SPMCTS_ERR_AB_SWITCH) rather than silently ignored.
+static constexpr bool c256_board3() { return false; }
+static constexpr bool wide_tails3() { return false; }
+static constexpr bool heads_co256() { return true; }
+static constexpr bool heads_co() { return true; }
+#endif
+// -5 when an A/B-library switch is set in a product build (read once)
+static int ab_switch_guard() {
+#ifdef SPMCTS_AB
+  return 0;
+#else
+  static const int rc = [] {
+    for (const char *n : {"SPMCTS_TOWER_CG", "SPMCTS_TOWER_RING", "SPMCTS_TOWER_C256", "SPMCTS_WIDE_TAILS", "SPMCTS_HEADS",
+                          "SPMCTS_HEADS_C256", "SPMCTS_TREE_BLOCK", "SPMCTS_EXPAND_CO"})
+      if (getenv(n)) return SPMCTS_ERR_AB_SWITCH;
+    return 0;
+  }();
+  return rc;
+#endif
 }
 
 // the instantiated tile sets of the device-count path, per board shape, channels and element type
@@ -1560,14 +1585,18 @@ static int forward_dev(int32_t width, int32_t height, int32_t channels, int32_t 
                       Cfg<128, 128, 7, 6, 2, 4, 0, 4, 1, false, false, E>>(planes_dev, count_dev, max_batch, n_blocks,
                                                                           weights_dev, bias_dev, features_dev, pack, s);
   if (width == 7 && height == 6 && channels == 256) {
-    // 6-board one-buffer edge tiles (tower_wide.h) with 3-board tails; SPMCTS_TOWER_C256=3: 3-board two-buffer tiles
+    // 6-board one-buffer edge tiles (tower_wide.h) with 3-board tails
     using K3 = Cfg<256, 128, 7, 6, 4, 4, 0, 4, 1, false, false, E>;
     using KW = Cfg<256, 256, 7, 6, 4, 4, 0, 2, 1, true, true, E, true>;
+#ifdef SPMCTS_AB
     if (c256_board3())
       return launch_dyn<K3, K3, K3>(planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, pack, s);
-    // packed launches (lanes beside each other) have a tail of < 6 boards: one 6-board tile takes it, and a
-    // kernel with the one-buffer code path only holds fewer registers (SPMCTS_WIDE_TAILS=3: 3-board tail code)
     if (pack && !wide_tails3())
+#else
+    // packed launches (lanes beside each other) have a tail of < 6 boards: one 6-board tile takes it, and a
+    // kernel with the one-buffer code path only holds fewer registers
+    if (pack)
+#endif
       return launch_dyn<KW, KW, KW>(planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, pack, s);
     return launch_dyn<KW, K3, K3>(planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, pack, s);
   }
@@ -1581,8 +1610,31 @@ static int forward_dev(int32_t width, int32_t height, int32_t channels, int32_t 
                                                                           weights_dev, bias_dev, features_dev, pack, s);
   return -2;
 }
+
+// the host-count path (a batch size known on the host): the same tile sets, split on the host
+template <class E>
+static int forward_host(int32_t width, int32_t height, int32_t channels, int32_t n_blocks, const char *pl, int32_t batch,
+                        const void *weights_dev, const float *bias_dev, char *ft, hipStream_t s) {
+  if (width == 7 && height == 6 && channels == 128)
+    return launch_split<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true, true, E>, Cfg<128, 192, 7, 6, 2, 4, 0, 4, 1, false, false, E>,
+                        Cfg<128, 128, 7, 6, 2, 4, 0, 4, 1, false, false, E>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+  if (width == 7 && height == 6 && channels == 256) {
+    using K3 = Cfg<256, 128, 7, 6, 4, 4, 0, 4, 1, false, false, E>;
+#ifdef SPMCTS_AB
+    if (c256_board3()) return launch<K3>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+#endif
+    return launch_split<Cfg<256, 256, 7, 6, 4, 4, 0, 2, 1, true, true, E, true>, K3, K3>(pl, batch, n_blocks, weights_dev,
+                                                                                       bias_dev, ft, s);
+  }
+  if (width == 3 && height == 3 && channels == 128)
+    return launch<Cfg<128, 256, 3, 3, 2, 4, 0, 4, 1, false, false, E>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+  if (width == 3 && height == 3 && channels == 256)
+    return launch<Cfg<256, 128, 3, 3, 4, 4, 0, 4, 1, false, false, E>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+  return -2;
+}
 }  // namespace tower
 
+#ifdef SPMCTS_AB
 namespace tower {
 // Ring trunk launch (tower_ring.h): full 6-board tiles only, for the C = 128 Connect4 net with at most
 // ring::MAX_CONVS / 2 blocks.  count == nullptr: the batch is max_batch.
@@ -1607,73 +1659,20 @@ static int launch_ring(const void *planes, const int32_t *count, int max_batch, 
 }
 
 // SPMCTS_TOWER_RING=1 runs the ring trunk for the C = 128 Connect4 net instead of the two-buffer trunk
-// (an A/B switch, read once; measured 3-6 % slower, DESIGN.md §4 "Weight ring in LDS")
+// (measured 3-6 % slower, DESIGN.md §4 "Round 3")
 static bool ring_enabled(int n_blocks) {
-  static int on = -1;
-  if (on < 0) {
-    const char *e = getenv("SPMCTS_TOWER_RING");
-    on = e ? atoi(e) != 0 : 0;
-  }
+  static const bool on = getenv("SPMCTS_TOWER_RING") && atoi(getenv("SPMCTS_TOWER_RING")) != 0;
   return on && 2 * n_blocks <= ring::MAX_CONVS;
 }
-}  // namespace tower
 
-extern "C" int spmcts_tower_forward_dev(int32_t width, int32_t height, int32_t channels, int32_t n_blocks,
-                                        const void *planes_dev, const int32_t *count_dev, int32_t max_batch,
-                                        const void *weights_dev, const float *bias_dev, void *features_dev,
-                                        int32_t flags, spmcts_stream stream) {
-  using namespace tower;
-  hipStream_t s = (hipStream_t)stream;
-  if (n_blocks < 0 || max_batch < 0 || !count_dev || (flags & ~(SPMCTS_TOWER_PACK | SPMCTS_TOWER_F16))) return -3;
-  if (max_batch == 0) return 0;
-  const bool pack = (flags & SPMCTS_TOWER_PACK) != 0;
-  if (width == 7 && height == 6 && channels == 128 && ring_enabled(n_blocks))
-    return (flags & SPMCTS_TOWER_F16 ? launch_ring<_Float16> : launch_ring<__bf16>)(
-        planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, s);
-  if (flags & SPMCTS_TOWER_F16)
-    return forward_dev<_Float16>(width, height, channels, n_blocks, planes_dev, count_dev, max_batch, weights_dev,
-                                 bias_dev, features_dev, pack, s);
-  return forward_dev<__bf16>(width, height, channels, n_blocks, planes_dev, count_dev, max_batch, weights_dev, bias_dev,
-                             features_dev, pack, s);
-}
-
-extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t channels, int32_t n_blocks,
-                                    const void *planes_dev, int32_t batch, const void *weights_dev,
-                                    const float *bias_dev, void *features_dev, int32_t flags, spmcts_stream stream) {
-  using namespace tower;
-  hipStream_t s = (hipStream_t)stream;
-  if (n_blocks < 0 || batch < 0 || (flags & ~SPMCTS_TOWER_F16)) return -3;
-  if (width == 7 && height == 6 && channels == 128 && ring_enabled(n_blocks) && !getenv("SPMCTS_TOWER_CG"))
-    return (flags & SPMCTS_TOWER_F16 ? launch_ring<_Float16> : launch_ring<__bf16>)(
-        planes_dev, nullptr, batch, n_blocks, weights_dev, bias_dev, features_dev, s);
-  if (flags & SPMCTS_TOWER_F16) {  // the shipped tile set only (the SPMCTS_TOWER_CG variants are bf16 timing studies)
-    const char *pl = (const char *)planes_dev;
-    char *ft = (char *)features_dev;
-    using E = _Float16;
-    if (width == 7 && height == 6 && channels == 128)
-      return launch_split<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true, true, E>, Cfg<128, 192, 7, 6, 2, 4, 0, 4, 1, false, false, E>,
-                          Cfg<128, 128, 7, 6, 2, 4, 0, 4, 1, false, false, E>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-    if (width == 7 && height == 6 && channels == 256) {
-      using K3 = Cfg<256, 128, 7, 6, 4, 4, 0, 4, 1, false, false, E>;
-      if (c256_board3()) return launch<K3>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-      return launch_split<Cfg<256, 256, 7, 6, 4, 4, 0, 2, 1, true, true, E, true>, K3, K3>(pl, batch, n_blocks,
-                                                                                         weights_dev, bias_dev, ft, s);
-    }
-    if (width == 3 && height == 3 && channels == 128)
-      return launch<Cfg<128, 256, 3, 3, 2, 4, 0, 4, 1, false, false, E>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-    if (width == 3 && height == 3 && channels == 256)
-      return launch<Cfg<256, 128, 3, 3, 4, 4, 0, 4, 1, false, false, E>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-    return -2;
-  }
-  static int cg = -1;
-  if (cg < 0) {
-    const char *e = getenv("SPMCTS_TOWER_CG");  // A/B switch for the wave split (2 = default)
-    cg = e ? atoi(e) : 2;
-  }
-  const char *pl = (const char *)planes_dev;
-  char *ft = (char *)features_dev;
+// SPMCTS_TOWER_CG=<code>: timing alternatives and ablations of the C = 128 trunk (bf16; some give wrong
+// results by design: DESIGN.md §4 has the measurements).  Returns 1 when no code is set.
+static int forward_ab(int32_t width, int32_t height, int32_t channels, int32_t n_blocks, const char *pl, int32_t batch,
+                      const void *weights_dev, const float *bias_dev, char *ft, hipStream_t s) {
+  static const int cg = getenv("SPMCTS_TOWER_CG") ? atoi(getenv("SPMCTS_TOWER_CG")) : -1;
+  if (cg < 0) return 1;
   if (width == 7 && height == 6 && channels == 128) {
-    switch (cg) {  // timing alternatives (SPMCTS_TOWER_CG); DESIGN.md §4 has the measurements
+    switch (cg) {
 #define ABLATE(X) \
       case 100 + X: return launch<Cfg<128, 256, 7, 6, 2, 4, X>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       ABLATE(0) ABLATE(1) ABLATE(2) ABLATE(4) ABLATE(8) ABLATE(16) ABLATE(24) ABLATE(31) ABLATE(64) ABLATE(128)
@@ -1697,23 +1696,59 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
       case 10: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);  // two tile sizes only
       case 15: return launch_split<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true>, Cfg<128, 192, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);  // column-major tiles without edge rows
       case 11: return launch_split<Cfg<128, 256, 7, 6, 2>, Cfg<128, 192, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);  // board-major full tiles
-      default: return launch_split<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true, true>, Cfg<128, 192, 7, 6, 2>, Cfg<128, 128, 7, 6, 2>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      default: return 1;
     }
   }
-  if (width == 7 && height == 6 && channels == 256) {  // as the device-count path
-    using K3 = Cfg<256, 128, 7, 6, 4>;
-    if (c256_board3()) return launch<K3>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-    if (cg == 254)  // timing alternative: the one-buffer trunk with a 4-deep weight ring (default 2)
-      return launch_split<Cfg<256, 256, 7, 6, 4, 4, 0, 4, 1, true, true, __bf16, true>, K3, K3>(pl, batch, n_blocks,
-                                                                                            weights_dev, bias_dev, ft, s);
-    return launch_split<Cfg<256, 256, 7, 6, 4, 4, 0, 2, 1, true, true, __bf16, true>, K3, K3>(pl, batch, n_blocks,
-                                                                                          weights_dev, bias_dev, ft, s);
+  if (width == 7 && height == 6 && channels == 256 && cg == 254)  // the one-buffer trunk with a 4-deep weight ring
+    return launch_split<Cfg<256, 256, 7, 6, 4, 4, 0, 4, 1, true, true, __bf16, true>, Cfg<256, 128, 7, 6, 4>,
+                        Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+  return 1;
+}
+}  // namespace tower
+#endif  // SPMCTS_AB
+
+extern "C" int spmcts_tower_forward_dev(int32_t width, int32_t height, int32_t channels, int32_t n_blocks,
+                                        const void *planes_dev, const int32_t *count_dev, int32_t max_batch,
+                                        const void *weights_dev, const float *bias_dev, void *features_dev,
+                                        int32_t flags, spmcts_stream stream) {
+  using namespace tower;
+  hipStream_t s = (hipStream_t)stream;
+  if (n_blocks < 0 || max_batch < 0 || !count_dev || (flags & ~(SPMCTS_TOWER_PACK | SPMCTS_TOWER_F16))) return -3;
+  if (const int g = ab_switch_guard()) return g;
+  if (max_batch == 0) return 0;
+  const bool pack = (flags & SPMCTS_TOWER_PACK) != 0;
+#ifdef SPMCTS_AB
+  if (width == 7 && height == 6 && channels == 128 && ring_enabled(n_blocks))
+    return (flags & SPMCTS_TOWER_F16 ? launch_ring<_Float16> : launch_ring<__bf16>)(
+        planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, s);
+#endif
+  if (flags & SPMCTS_TOWER_F16)
+    return forward_dev<_Float16>(width, height, channels, n_blocks, planes_dev, count_dev, max_batch, weights_dev,
+                                 bias_dev, features_dev, pack, s);
+  return forward_dev<__bf16>(width, height, channels, n_blocks, planes_dev, count_dev, max_batch, weights_dev, bias_dev,
+                             features_dev, pack, s);
+}
+
+extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t channels, int32_t n_blocks,
+                                    const void *planes_dev, int32_t batch, const void *weights_dev,
+                                    const float *bias_dev, void *features_dev, int32_t flags, spmcts_stream stream) {
+  using namespace tower;
+  hipStream_t s = (hipStream_t)stream;
+  if (n_blocks < 0 || batch < 0 || (flags & ~SPMCTS_TOWER_F16)) return -3;
+  if (const int g = ab_switch_guard()) return g;
+  const char *pl = (const char *)planes_dev;
+  char *ft = (char *)features_dev;
+#ifdef SPMCTS_AB
+  if (!(flags & SPMCTS_TOWER_F16)) {
+    if (width == 7 && height == 6 && channels == 128 && ring_enabled(n_blocks) && !getenv("SPMCTS_TOWER_CG"))
+      return launch_ring<__bf16>(planes_dev, nullptr, batch, n_blocks, weights_dev, bias_dev, features_dev, s);
+    const int rc = forward_ab(width, height, channels, n_blocks, pl, batch, weights_dev, bias_dev, ft, s);
+    if (rc != 1) return rc;
   }
-  if (width == 3 && height == 3 && channels == 128)
-    return launch<Cfg<128, 256, 3, 3>>(planes_dev, batch, n_blocks, weights_dev, bias_dev, features_dev, s);
-  if (width == 3 && height == 3 && channels == 256)
-    return launch<Cfg<256, 128, 3, 3>>(planes_dev, batch, n_blocks, weights_dev, bias_dev, features_dev, s);
-  return -2;
+#endif
+  if (flags & SPMCTS_TOWER_F16)
+    return forward_host<_Float16>(width, height, channels, n_blocks, pl, batch, weights_dev, bias_dev, ft, s);
+  return forward_host<__bf16>(width, height, channels, n_blocks, pl, batch, weights_dev, bias_dev, ft, s);
 }
 
 template <class E>
@@ -1723,22 +1758,27 @@ static int tower_heads(int32_t width, int32_t height, int32_t channels, int32_t 
   using namespace tower;
   hipStream_t s = (hipStream_t)stream;
   if (batch <= 0) return batch < 0 ? -3 : 0;
-  // SPMCTS_HEADS=lds: the LDS-staged k_heads (A/B switch, read per call); default the co-resident k_heads_co
-  const char *he = getenv("SPMCTS_HEADS");
-  const int co = (he && strcmp(he, "lds") == 0) ? 0 : 1;
-#define HEADS(FF, CELLS, A)                                                                                   \
-  do {                                                                                                        \
-  /* C = 256 (FF = 64): two value passes of 2 tiles in 96 registers, beside the C = 256 trunk */          \
-  if (co && (FF == 32 || heads_co256()))                                                                     \
-    hipLaunchKernelGGL((k_heads_co<FF, CELLS, A, E, 5, FF == 64 ? 2 : HeadsCfg<FF, CELLS, A>::VTW>),          \
-                       dim3((batch + 31) / 32), dim3(256), 0, s, (const uint16_t *)features_dev, batch,       \
-                       count_dev, (const bf16x8 *)head_w_dev, head_b_dev, probs_dev, values_dev);             \
-  else                                                                                                        \
-    hipLaunchKernelGGL((k_heads<FF, CELLS, A, E>), dim3((batch + HeadsCfg<FF, CELLS, A>::BOARDS - 1) /        \
-                                                     HeadsCfg<FF, CELLS, A>::BOARDS), dim3(256), 0, s,         \
-                         (const uint16_t *)features_dev, batch, count_dev, (const bf16x8 *)head_w_dev, head_b_dev,\
-                       probs_dev, values_dev);                                                                \
+  if (const int g = ab_switch_guard()) return g;
+  // the co-resident k_heads_co (C = 256, FF = 64: two value passes of 2 tiles in 96 registers, beside the
+  // C = 256 trunk); the A/B library's SPMCTS_HEADS=lds / SPMCTS_HEADS_C256=lds select the LDS-staged k_heads
+#define HEADS_CO(FF, CELLS, A)                                                                              \
+  hipLaunchKernelGGL((k_heads_co<FF, CELLS, A, E, 5, FF == 64 ? 2 : HeadsCfg<FF, CELLS, A>::VTW>),          \
+                     dim3((batch + 31) / 32), dim3(256), 0, s, (const uint16_t *)features_dev, batch,       \
+                     count_dev, (const bf16x8 *)head_w_dev, head_b_dev, probs_dev, values_dev)
+#ifdef SPMCTS_AB
+#define HEADS(FF, CELLS, A)                                                                                 \
+  do {                                                                                                      \
+    if (heads_co() && (FF == 32 || heads_co256()))                                                         \
+      HEADS_CO(FF, CELLS, A);                                                                               \
+    else                                                                                                    \
+      hipLaunchKernelGGL((k_heads<FF, CELLS, A, E>), dim3((batch + HeadsCfg<FF, CELLS, A>::BOARDS - 1) /    \
+                                                       HeadsCfg<FF, CELLS, A>::BOARDS), dim3(256), 0, s,     \
+                         (const uint16_t *)features_dev, batch, count_dev, (const bf16x8 *)head_w_dev,      \
+                         head_b_dev, probs_dev, values_dev);                                                \
   } while (0)
+#else
+#define HEADS(FF, CELLS, A) HEADS_CO(FF, CELLS, A)
+#endif
   if (width == 7 && height == 6 && actions == 7 && channels == 128)
     HEADS(32, 42, 7);
   else if (width == 7 && height == 6 && actions == 7 && channels == 256)
@@ -1750,6 +1790,7 @@ static int tower_heads(int32_t width, int32_t height, int32_t channels, int32_t 
   else
     return -2;
 #undef HEADS
+#undef HEADS_CO
   return hipGetLastError() == hipSuccess ? 0 : -11;
 }
 

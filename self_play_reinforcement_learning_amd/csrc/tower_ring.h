@@ -389,7 +389,7 @@ __device__ __forceinline__ void ring_tile(char *smem, const __bf16 *planes, int 
   for (int row = tid; row < K::ROWS; row += K::THREADS) {
     const int board = board0 + K::row_board(row);
     uint16_t *dst = (uint16_t *)(smem + row * K::RS);
-    const bool ok = row < K::VROWS && board < batch;
+    const bool ok = K::row_ok(row) && board < batch;
     const size_t src = ((size_t)board * K::CELLS + K::row_cell(row)) * 3;
 #pragma unroll
     for (int c = 0; c < 16; ++c) dst[c] = (ok && c < 3) ? K::from_bf16(planes[src + c]) : (uint16_t)0;

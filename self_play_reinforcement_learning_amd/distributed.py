@@ -322,12 +322,16 @@ def _spawned_rank(rank, world, port, fn, args, kwargs):
     fn(*args, **kwargs)
 
 
-def spawn_ranks(fn, n, *args, **kwargs):
+def spawn_ranks(fn, n, *args, timeout=None, **kwargs):
     """Run fn(*args, **kwargs) in n fresh processes (spawn), rank r with torchrun's environment: how
     SelfPlayScheduler starts one process per GPU itself, as the reference's scheduler starts its
     own worker processes (self_play_parallel.py:95-171).  fn and its arguments must pickle; CPU
-    tensors travel by shared memory.  Raises if any rank fails."""
+    tensors travel by shared memory.  The ranks are watched together: the first rank that exits
+    non-zero gets the others terminated at once (a survivor would otherwise wait in a collective for
+    the backend's timeout), and RuntimeError is raised.  `timeout` (seconds, None = none) bounds the
+    whole run the same way."""
     import multiprocessing as mp
+    from multiprocessing.connection import wait
 
     ctx = mp.get_context("spawn")
     port = free_port()
@@ -335,12 +339,44 @@ def spawn_ranks(fn, n, *args, **kwargs):
     for p in procs:
         p.start()
     failed = []
-    for r, p in enumerate(procs):
-        p.join()
-        if p.exitcode:
-            failed.append((r, p.exitcode))
-            for q in procs:
-                if q.is_alive():
-                    q.terminate()
+    t_end = None if timeout is None else time.monotonic() + timeout
+    live = {p.sentinel: (r, p) for r, p in enumerate(procs)}
+    try:
+        while live:
+            left = None if t_end is None else max(0.0, t_end - time.monotonic())
+            ready = wait(list(live), timeout=left)
+            if not ready:
+                failed.append(("timeout", timeout))
+                break
+            for s in ready:
+                r, p = live.pop(s)
+                p.join()
+                if p.exitcode:
+                    failed.append((r, p.exitcode))
+            if failed:
+                break
+    finally:
+        for r, p in enumerate(procs):
+            if p.is_alive():
+                p.terminate()
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+                p.join()
     if failed:
         raise RuntimeError(f"rank process(es) failed: {failed}")
+
+
+def rank_report(values):
+    """All-gather one float64 vector per rank (every rank gets the [world, len] table; a one-row
+    table without a process group): the per-rank lines of bench.py's N-rank report (positions/s,
+    timed seconds, exchange rounds and their cost), so a scaling record shows stragglers directly."""
+    t = torch.as_tensor([float(x) for x in values], dtype=torch.float64)
+    if not is_distributed():
+        return [t.tolist()]
+    dev = _comm_device()
+    t = t.to(dev)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [o.cpu().tolist() for o in out]

@@ -85,13 +85,14 @@ def union_ms(intervals):
 
 class SelfPlayEngine:
     def __init__(self, game, network, n_games=4096, iterations=200, alpha=1.0, strong_play=False, evaluate=False,
-                 seed=0, subsequence0=None, rng="philox", max_games=None, device=None, dtype=torch.bfloat16,
+                 seed=0, subsequence0=None, rng="philox", max_games=None, device=None, dtype=torch.float16,
                  leaf_layout="nhwc", cpuct=4.0, x_noise=0.25, blocks_per_tree=0, bucket=256, opponent=None,
                  opponent_iterations=None, record=True, search_threads=1, leaf_dedup=None, opponent_alpha=None,
                  opponent_strong_play=None, opponent_search_threads=None):
         """opponent_alpha / opponent_strong_play / opponent_search_threads: the opposing MCTS side's own
         search settings (evaluation games: each side is built from its own container's kwargs,
-        selfplayworker.py:71-81); None = the policy's."""
+        selfplayworker.py:71-81); None = the policy's.  dtype: the fused trunk's element type, fp16 by
+        default (the reference's inference autocast, inference_worker.py:114-119) or bf16."""
         self.game = game
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.evaluator = make_evaluator(network, game, device=self.device, dtype=dtype, leaf_layout=leaf_layout)
@@ -364,7 +365,8 @@ class SelfPlayEngine:
             plies += 1
             if on_ply is not None:
                 on_ply(self)
-            r = ex.end_ply(self.stats_vector, done=self.games_done >= target)
+            # the statistics are read (a host sync on the device counters) only for a real exchange round
+            r = ex.end_ply(self.stats_vector if distributed.is_distributed() else None, done=self.games_done >= target)
             if r is not None and r[0]:
                 break
         self._started = self._limit
@@ -391,6 +393,12 @@ class SelfPlayEngine:
 
     def counters(self):
         return self.arena.counters()
+
+    @property
+    def weights_snapshot(self):
+        """True when every leaf evaluator reads its own copy of the weights (Evaluator.snapshot), so
+        SGD steps may run on another stream beside this engine's plies."""
+        return all(getattr(ev, "snapshot", False) for ev in (self.evaluator, self.evaluator1) if ev is not None)
 
     def stats_vector(self):
         """[games, moves, first w/d/l, second w/d/l] for the episode-end all_reduce."""
@@ -573,12 +581,17 @@ class LanedEngine:
             plies += 1
             if on_ply is not None:
                 on_ply(self)
-            r = ex.end_ply(self.stats_vector, done=all(e.games_done >= t for e, t in zip(self.lanes, targets)))
+            r = ex.end_ply(self.stats_vector if distributed.is_distributed() else None,
+                           done=all(e.games_done >= t for e, t in zip(self.lanes, targets)))
             if r is not None and r[0]:
                 break
         for e in self.lanes:
             e._started = e._limit
         return plies
+
+    @property
+    def weights_snapshot(self):
+        return all(e.weights_snapshot for e in self.lanes)
 
     def counters(self):
         cs = self._each(lambda e: e.counters())

@@ -54,10 +54,15 @@ class DeviceTableNet:
 
 
 class Evaluator:
-    """callable(leaves [n, ...]) -> (probs f32 [n, A] contiguous, values f32 [n])."""
+    """callable(leaves [n, ...]) -> (probs f32 [n, A] contiguous, values f32 [n]).
+
+    `snapshot`: the evaluator reads its own copy of the weights (refreshed by refresh()), never the
+    live module's parameters / BatchNorm buffers, so optimizer steps on another stream may run beside
+    its evaluations (SelfPlayScheduler's overlapped trainer); False = it reads the live module."""
 
     leaf_format = "bf16"
     leaf_layout = "nchw"
+    snapshot = False
 
     def empty_root_input(self, W, H, device):
         """The input row of the empty board (`network(base_state)`, mcts.py:167-168)."""
@@ -72,6 +77,8 @@ class Evaluator:
 
 
 class TableEvaluator(Evaluator):
+    snapshot = True  # no trainable weights
+
     def __init__(self, net, leaf_format="f32", leaf_layout="nchw"):
         self.net = net
         self.leaf_format, self.leaf_layout = leaf_format, leaf_layout
@@ -90,6 +97,12 @@ class TowerEvaluator(Evaluator):
         self.leaf_layout = leaf_layout
         self.device = device
         self.refresh()
+
+    @property
+    def snapshot(self):
+        # bf16 / fp16 folding copies every tensor; in fp32 `.to(float32)` can alias the live bias and
+        # linear_output tensors
+        return self.dtype != torch.float32
 
     @torch.no_grad()
     def refresh(self):
@@ -219,6 +232,7 @@ class HipTowerEvaluator(Evaluator):
     leaf_format = "bf16"
     leaf_layout = "nhwc"
     bucket = 1  # the HIP kernels take any batch size; no shape padding needed
+    snapshot = True  # packed weight / bias blobs (refresh())
 
     def __init__(self, tower, device=None, fused_heads=True, dtype=torch.bfloat16):
         """fused_heads: True = MFMA heads kernel (deterministic, batch-independent), "gemm" =
@@ -237,6 +251,17 @@ class HipTowerEvaluator(Evaluator):
         self.W, self.H, self.A = tower.width, tower.height, tower.action_size
         if not _lib.lib().spmcts_tower_supported(self.W, self.H, self.C):
             raise ValueError(f"fused tower not instantiated for {self.W}x{self.H} boards, {self.C} channels")
+        self.refresh()
+
+    def set_dtype(self, dtype):
+        """Repack the weights for the other trunk element type (bf16 <-> fp16) and drop the device
+        buffers (reallocated at the next forward); the caller refreshes its root prior
+        (SelfPlayEngine.refresh_network)."""
+        if dtype not in (torch.bfloat16, torch.float16):
+            raise ValueError(f"fused tower dtype must be bfloat16 or float16, not {dtype}")
+        self.dtype = dtype
+        self.flags = self._lib.TOWER_F16 if dtype == torch.float16 else 0
+        self._dev_bufs = None
         self.refresh()
 
     @staticmethod

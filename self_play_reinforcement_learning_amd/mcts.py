@@ -101,7 +101,8 @@ class MCTreeSearch(Policy):
         # network is an InferenceProxy (mcts.py:154, :328-331); False: its sequential mode
         self.threading = bool(threading)
         k = int(thread_count) if self.threading and thread_count and thread_count > 1 else 1
-        self._evaluator = make_evaluator(network, self.game, device=self.device)
+        # fp16 trunk: the reference's inference autocast dtype (inference_worker.py:114-119)
+        self._evaluator = make_evaluator(network, self.game, device=self.device, dtype=torch.float16)
         if seed is None:
             seed = int(np.random.randint(0, 2**31 - 1))
         self._arena = Arena(self.game, n_trees=1, n_games=0, iterations=iterations, rng=rng, seed=seed,

@@ -24,7 +24,8 @@ signatures.  What changes is underneath:
 Multi-GPU: one process per GPU.  Under torchrun (WORLD_SIZE > 1) every rank plays
 its own shard of games; Move records and episode statistics are gathered to
 rank 0 (distributed.py).  Without torchrun, `train_model` / `compare_models`
-start the rank processes themselves (`gpus=`; default: every visible GPU), as
+start the rank processes themselves when asked (`gpus=N` or `gpus="all"`; the
+default runs in this process, on the constructor's device), as
 the reference's scheduler starts its own worker processes
 (self_play_parallel.py:95-171, num_workers = cpu_count()): the children rebuild
 this scheduler from its constructor arguments (networks copied to the host),
@@ -92,7 +93,7 @@ class SelfPlayScheduler:
                  save_dir="saves", epoch_length=500, initial_games=64, lr=0.001, stagger=False, evaluation_games=100,
                  evaluation_network=None, stagger_mem_step=5000, deduplicate=False, update_delay=0.01,
                  self_play=None, n_games=None, device=None, seed=0, updates_per_ply=4, lanes=None, exchange_every=8,
-                 gpus=None, start_time=None, overlap_training=True, train_autocast=True):
+                 gpus=None, start_time=None, overlap_training=True, train_autocast=True, train_graph=True):
         # constructor arguments, for rank processes started by this scheduler (_run_ranks)
         self._init_kwargs = {k: v for k, v in locals().items() if k not in ("self", "__class__")}
         self.policy_container = policy_container
@@ -119,6 +120,8 @@ class SelfPlayScheduler:
         # the UpdateWorker's update_from_memory runs under torch.cuda.amp.autocast() (fp16 on CUDA, no
         # GradScaler; updateworker.py:148); False trains in fp32
         self.train_autocast = train_autocast
+        # the trainer's update captured as one HIP graph and replayed per step (_Trainer graph=True)
+        self.train_graph = train_graph
         self.exchange_every = exchange_every  # plies per episode-batch exchange round (distributed.MoveExchange)
         # >1: LanedEngine (arenas on separate HIP streams, each a complete arena); None = 2 lanes for
         # arenas of >= 1,024 games, where the overlap pays (bench.py), else one arena
@@ -200,10 +203,19 @@ class SelfPlayScheduler:
         self.trainer = _Trainer(self.network, optim, memory_size=kw.get("memory_size", 200000),
                                 batch_size=kw.get("batch_size", 64), min_memory=kw.get("min_memory", 20000),
                                 q_average=kw.get("q_average", True), device=self.device, W=self.W, H=self.H,
-                                A=self.A, overlap=self.overlap_training, autocast=self.train_autocast)
+                                A=self.A, overlap=self._overlap_ok(), autocast=self.train_autocast,
+                                graph=self.train_graph)
         if resume_model:
             self._load_latest(prev_run=True)
         return self.trainer, None, None
+
+    def _overlap_ok(self):
+        """SGD steps on the trainer's own stream beside the plies only when the self-play engine's
+        evaluators hold a snapshot of the weights (the fused HIP trunk's packed blobs, a bf16 / fp16
+        folded tower): an evaluator that reads the live module (ModuleEvaluator, an fp32 folded tower)
+        would race with optimizer.step, so its steps stay on the plies' stream, in order."""
+        eng = self.engine
+        return bool(self.overlap_training and eng is not None and getattr(eng, "weights_snapshot", False))
 
     def _load_latest(self, prev_run=False):
         from glob import glob
@@ -264,11 +276,15 @@ class SelfPlayScheduler:
     # ------------------------------------------------------------------ one process per GPU
     def _ranks(self, gpus):
         """How many rank processes this call starts: 1 (run here) inside a launched job; else `gpus`
-        (the call's, then the constructor's; None = every visible GPU)."""
+        (the call's, then the constructor's; None = 1, in this process on the constructor's device;
+        "all" = every visible GPU).  After a multi-rank run this scheduler holds no trainer or engine
+        state: only its network, loaded from the last checkpoint (train_model)."""
         if D.in_launched_job() or D.is_distributed():
             return 1
         n = gpus if gpus is not None else self.gpus
         if n is None:
+            return 1
+        if n == "all":
             n = torch.cuda.device_count()  # counting devices does not initialise the GPU
         return max(1, int(n))
 
@@ -302,9 +318,8 @@ class SelfPlayScheduler:
 
     def train_model(self, num_epochs=10, resume_model=False, resume_memory=False, num_workers=None,
                     threads_per_worker=8, inference_proxy=True, gpus=None):
-        """self_play_parallel.py:213-291.  gpus > 1 (default: every visible GPU) outside a launched
-        job: one rank process per GPU (_run_ranks); this scheduler's network then holds the final
-        checkpoint's weights."""
+        """self_play_parallel.py:213-291.  gpus > 1 (or "all") outside a launched job: one rank process
+        per GPU (_run_ranks); this scheduler's network then holds the final checkpoint's weights."""
         n = self._ranks(gpus)
         if n > 1:
             self._run_ranks(n, "train_model", dict(num_epochs=num_epochs, resume_model=resume_model,
@@ -483,10 +498,20 @@ class _Trainer:
     returns without a host synchronisation, so the SGD kernels run beside the arena's next ply
     (self-play evaluates leaves with its own packed copy of the epoch-start weights, refreshed at
     epoch boundaries).  `sync()` makes the current stream wait for the queued steps: before replay
-    rows are overwritten and before the weights are read (checkpoint, weight refresh)."""
+    rows are overwritten and before the weights are read (checkpoint, weight refresh).
+
+    `graph` (CUDA device, default on): after `GRAPH_WARMUP` eager steps the whole update -- forward,
+    AZ loss, backward, SGD/momentum/weight-decay step, BatchNorm statistics, dropout -- is captured
+    once as a HIP graph (torch.cuda.CUDAGraph) and replayed per step: one launch instead of ~600
+    small kernels, whose launch costs dominated a batch-64 step of ResNet-128x20.  The sampled batch
+    (uniform without replacement, on the device) is copied into the graph's static input buffers
+    first.  The graph is re-captured when the learning rate changes (ReduceLROnPlateau), since the
+    captured optimizer kernels hold the rate as a constant."""
+
+    GRAPH_WARMUP = 3
 
     def __init__(self, network, optim, memory_size, batch_size, min_memory, q_average, device, W=7, H=6, A=7,
-                 train_mode=True, overlap=True, autocast=False):
+                 train_mode=True, overlap=True, autocast=False, graph=True):
         from .replay import DeviceReplay
 
         dev = torch.device(device) if device is not None else torch.device("cpu")
@@ -507,6 +532,13 @@ class _Trainer:
         self.autocast = bool(autocast) and dev.type == "cuda"
         self.scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optim, "max", patience=15, factor=0.5,
                                                                     min_lr=0.00001, cooldown=5)
+        self.graph = bool(graph) and dev.type == "cuda"
+        self._g = None          # the captured step (torch.cuda.CUDAGraph)
+        self._g_key = None      # (lr of every param group, autocast, train_mode) it was captured with
+        self._g_in = None       # its static inputs (s, z, pi, q)
+        self._g_loss = None     # its static loss output
+        self._eager_steps = 0   # eager steps since the last (re)capture request
+        self.graph_captures = 0
 
     def pull(self, queue):
         while not queue.empty():
@@ -520,10 +552,14 @@ class _Trainer:
             return None
         self.steps += 1
         if self.stream is None:
+            if self.graph:
+                self.last_loss = self._step_graphed(*self.memory.sample_batch(self.batch_size))
+                return float(self.last_loss)
             return self.train_batch(*self.memory.sample_batch(self.batch_size))
         self.stream.wait_stream(torch.cuda.current_stream(self.stream.device))
         with torch.cuda.stream(self.stream):
-            self.last_loss = self._train_step(*self.memory.sample_batch(self.batch_size))
+            batch = self.memory.sample_batch(self.batch_size)
+            self.last_loss = self._step_graphed(*batch) if self.graph else self._train_step(*batch)
         return self.last_loss
 
     def sync(self):
@@ -540,6 +576,46 @@ class _Trainer:
             self.optim.step()
         self.network.eval()
         return loss.detach()
+
+    def _graph_key(self):
+        return (tuple(float(g["lr"]) for g in self.optim.param_groups), self.autocast, self.train_mode)
+
+    def _step_graphed(self, s, z, pi, q):
+        """One update through the captured graph (on the current stream).  The first GRAPH_WARMUP
+        steps after a (re)capture request run eagerly -- they are real updates, and they create the
+        optimizer's momentum buffers and let the convolution library settle its kernel choice -- then
+        the update is captured and every later step is a copy of the batch + one graph replay."""
+        key = self._graph_key()
+        if self._g is not None and key != self._g_key:
+            self._g = None  # learning rate changed: the captured SGD kernels hold the old one
+            self._eager_steps = 0
+        if self._g is None and self._eager_steps < self.GRAPH_WARMUP:
+            self._eager_steps += 1
+            return self._train_step(s, z, pi, q)
+        if self._g is None:
+            self._capture(s, z, pi, q)
+            self._g_key = key
+        for dst, src in zip(self._g_in, (s, z, pi, q)):
+            dst.copy_(src)
+        self._g.replay()
+        self.network.eval()  # the captured step ran in train mode; module flags are host state
+        return self._g_loss.detach()
+
+    def _capture(self, s, z, pi, q):
+        self._g_in = tuple(t.detach().clone() for t in (s, z, pi, q))
+        g = torch.cuda.CUDAGraph()
+        self.network.train(self.train_mode)
+        self.optim.zero_grad(set_to_none=True)  # the gradients are allocated inside the graph's pool
+        # captured on torch's side stream (it synchronises the device once, here); replays run on the
+        # caller's current stream
+        with torch.cuda.graph(g):
+            with torch.autocast("cuda", dtype=torch.float16, enabled=self.autocast, cache_enabled=False):
+                loss = az_loss(self.network, *self._g_in, self.q_average)
+            loss.backward()
+            self.optim.step()
+        self.network.eval()
+        self._g, self._g_loss = g, loss
+        self.graph_captures += 1
 
     def train_batch(self, s, z, pi, q):
         """loss (mcts.py:234-252, via mcts.az_loss) -> zero_grad -> backward -> SGD step, with the

@@ -338,6 +338,86 @@ def test_spawn_ranks(tmp_path):
         D.spawn_ranks(_spawn_target, 2, str(tmp_path), "fail")
 
 
+def _spawn_slow_or_fail(out):
+    """Rank 1 fails at once; rank 0 would wait for a minute (as in a collective whose peer is gone)."""
+    import time
+
+    rank = int(os.environ["RANK"])
+    if rank == 1:
+        raise SystemExit(7)
+    time.sleep(60)
+
+
+def test_spawn_ranks_fails_fast(tmp_path):
+    """A rank that dies while rank 0 is still busy ends the whole call at once (the survivors are
+    terminated), not after rank 0 finishes or the backend's collective timeout."""
+    import time
+
+    t0 = time.monotonic()
+    with pytest.raises(RuntimeError, match=r"\(1, 7\)"):
+        D.spawn_ranks(_spawn_slow_or_fail, 2, str(tmp_path))
+    assert time.monotonic() - t0 < 45
+
+
+def _report_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      SPMCTS_DIST_INIT="file://" + port)
+    D.init_from_env(backend="gloo")
+    ex = D.MoveExchange(42, 7, every=2)
+    for ply in range(4):
+        ex.stage(_moves(rank + ply, rank + 1))
+        ex.end_ply(lambda: [ply], done=False)
+    rep = D.rank_report([100.0 * (rank + 1), 2.0, ex.rounds, ex.seconds / max(1, ex.rounds) * 1e3, ex.rows_gathered])
+    q.put((rank, rep))
+    torch.distributed.destroy_process_group()
+
+
+def test_rank_report_gloo():
+    """bench.py's per-rank lines: every rank gets every rank's row (positions/s, timed seconds,
+    exchange rounds, ms per round, rows received), in rank order."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_report_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == res[1]
+    rows = res[0]
+    assert [r[0] for r in rows] == [100.0, 200.0] and all(r[1] == 2.0 for r in rows)
+    assert all(r[2] == 2 and r[3] >= 0 for r in rows)  # two exchange rounds (every 2 of 4 plies)
+    assert rows[0][4] == 4 * 1 + 4 * 2 and rows[1][4] == 0  # rows reach rank 0 only
+    assert D.rank_report([1.0, 2.0]) == [[1.0, 2.0]]  # no process group: this process's row
+
+
+def test_overlap_needs_weight_snapshot():
+    """The trainer's own stream is used only when every self-play evaluator reads a snapshot of the
+    weights; an evaluator on the live module keeps the SGD steps on the plies' stream (no race)."""
+    import types
+
+    from self_play_reinforcement_learning_amd import evaluator as E
+    from self_play_reinforcement_learning_amd.engine import SelfPlayEngine
+    from self_play_reinforcement_learning_amd.self_play_parallel import SelfPlayScheduler
+
+    assert E.HipTowerEvaluator.snapshot and E.TableEvaluator.snapshot
+    assert not E.ModuleEvaluator.snapshot and not E.CallableEvaluator.snapshot
+    fake = types.SimpleNamespace(evaluator=E.ModuleEvaluator(torch.nn.Identity()), evaluator1=None)
+    assert SelfPlayEngine.weights_snapshot.fget(fake) is False
+    fake.evaluator = E.TableEvaluator(None)
+    assert SelfPlayEngine.weights_snapshot.fget(fake) is True
+    sp = SelfPlayScheduler.__new__(SelfPlayScheduler)
+    sp.overlap_training = True
+    sp.engine = types.SimpleNamespace(weights_snapshot=False)
+    assert not sp._overlap_ok()
+    sp.engine = types.SimpleNamespace(weights_snapshot=True)
+    assert sp._overlap_ok()
+    sp.overlap_training = False
+    assert not sp._overlap_ok()
+
+
 def _exchange_worker(rank, world, port, q):
     # SPMCTS_DIST_SINGLE: world size 1 runs the same collectives (the 1-GPU RCCL rehearsal's mode)
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
@@ -397,7 +477,8 @@ def test_move_exchange_rounds_gloo(world):
 
 def test_scheduler_rank_count_and_spawn_kwargs(tmp_path, monkeypatch):
     """SelfPlayScheduler(gpus=...): how many rank processes train_model / compare_models start (1 inside
-    a launched job; else the call's gpus, the constructor's, or every visible GPU), and the constructor
+    a launched job; else the call's gpus, the constructor's, 1 (in-process) by default, every visible GPU
+    for gpus="all"), and the constructor
     arguments the ranks rebuild it from (networks as host copies, one start_time, gpus=1) pickle."""
     import pickle
 
@@ -416,7 +497,8 @@ def test_scheduler_rank_count_and_spawn_kwargs(tmp_path, monkeypatch):
     monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
     assert sp._ranks(None) == 3 and sp._ranks(2) == 2 and sp._ranks(1) == 1
     sp.gpus = None
-    assert sp._ranks(None) == 8
+    assert sp._ranks(None) == 1  # in this process unless asked
+    assert sp._ranks("all") == 8
     monkeypatch.setenv("WORLD_SIZE", "8")
     monkeypatch.setenv("RANK", "0")
     assert sp._ranks(4) == 1  # already one rank of a launched job

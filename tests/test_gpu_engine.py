@@ -150,7 +150,7 @@ def test_mcts_search_after_update_uses_new_weights():
     pol.update_from_memory()  # one SGD step changes the module's weights
     pol()  # no reset in between: the search must see them
     after, _ = pol._evaluator(x)
-    fresh, _ = HipTowerEvaluator(net)(x)
+    fresh, _ = HipTowerEvaluator(net, dtype=pol._evaluator.dtype)(x)
     assert not torch.equal(before, after)
     assert torch.equal(after, fresh)
 
@@ -180,6 +180,72 @@ def test_trainer_steps_overlap_without_host_sync(tmp_path):
         out.append({k: v.clone() for k, v in net.state_dict().items()})
     for k in out[0]:  # same steps in the same order (backward kernels may differ in reduction order)
         torch.testing.assert_close(out[0][k], out[1][k], rtol=1e-4, atol=1e-6, msg=k)
+
+
+@pytest.mark.parametrize("autocast", [False, True])
+def test_trainer_graph_matches_eager_steps(autocast):
+    """The captured-graph update (_Trainer(graph=True): forward, AZ loss, backward and the SGD step as
+    one HIP graph replayed per step) gives the weights of the same updates run eagerly, step for step:
+    3 eager warm-up steps, the capture, replays; a learning-rate change (ReduceLROnPlateau) re-captures
+    and the new rate takes effect.  Eval-mode dropout (the masks' RNG is drawn differently inside a graph)."""
+    from self_play_reinforcement_learning_amd.modules import ResidualTower
+    from self_play_reinforcement_learning_amd.self_play_parallel import _Trainer
+
+    g = torch.Generator().manual_seed(7)
+    rows = dict(state=torch.randint(-1, 2, (512, 42), dtype=torch.int8, generator=g),
+                tree_probs=torch.softmax(torch.randn(512, 7, generator=g), 1),
+                q=torch.rand(512, dtype=torch.float64, generator=g) - 0.5,
+                z=torch.randint(-1, 2, (512,), generator=g).float())
+    out, batches = [], None
+    for graph in (False, True):
+        torch.manual_seed(0)
+        net = ResidualTower(7, 6, 7, num_blocks=2, filter_factor=16).cuda()
+        opt = torch.optim.SGD(net.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+        tr = _Trainer(net, opt, memory_size=1000, batch_size=64, min_memory=0, q_average=True, device="cuda",
+                      overlap=False, autocast=autocast, train_mode=False, graph=graph)
+        tr.memory.add_moves(rows)
+        if batches is None:
+            torch.manual_seed(11)
+            batches = [tr.memory.sample_batch(64) for _ in range(10)]
+        losses = []
+        for i, b in enumerate(batches):
+            if i == 6:
+                opt.param_groups[0]["lr"] = 0.002  # as ReduceLROnPlateau does
+            losses.append(float(tr._step_graphed(*b) if graph else tr._train_step(*b)))
+        torch.cuda.synchronize()
+        if graph:
+            assert tr.graph_captures == 2  # steps 3 and 9 (after 3 eager steps each time)
+        out.append(({k: v.clone() for k, v in net.state_dict().items()}, losses))
+    (w0, l0), (w1, l1) = out
+    assert all(math.isfinite(x) for x in l1)
+    assert max(abs(a - b) for a, b in zip(l0, l1)) < 1e-4 * max(abs(x) for x in l0), (l0, l1)
+    for k in w0:
+        torch.testing.assert_close(w0[k], w1[k], rtol=1e-4, atol=1e-6, msg=k)
+
+
+def test_trainer_graph_train_mode_replays_run():
+    """In train mode (dropout, BatchNorm batch statistics) every replay is a real update: the weights
+    move on each step and BatchNorm's step counter counts every step, eager and replayed."""
+    from self_play_reinforcement_learning_amd.modules import ResidualTower
+    from self_play_reinforcement_learning_amd.self_play_parallel import _Trainer
+
+    torch.manual_seed(0)
+    net = ResidualTower(7, 6, 7, num_blocks=2, filter_factor=16).cuda()
+    tr = _Trainer(net, torch.optim.SGD(net.parameters(), lr=0.01, momentum=0.9), memory_size=1000, batch_size=64,
+                  min_memory=0, q_average=True, device="cuda", overlap=True, autocast=True)
+    g = torch.Generator().manual_seed(1)
+    tr.memory.add_moves(dict(state=torch.randint(-1, 2, (256, 42), dtype=torch.int8, generator=g),
+                             tree_probs=torch.full((256, 7), 1 / 7), q=torch.zeros(256, dtype=torch.float64),
+                             z=torch.randint(-1, 2, (256,), generator=g).float()))
+    prev = net.conv1.weight.detach().clone()
+    for i in range(8):
+        loss = tr.step()
+        tr.sync()
+        torch.cuda.synchronize()
+        assert math.isfinite(float(loss))
+        assert not torch.equal(prev, net.conv1.weight), i
+        prev = net.conv1.weight.detach().clone()
+    assert tr.graph_captures == 1 and int(net.bn1.num_batches_tracked) == 8
 
 
 def test_trainer_autocast_matches_fp32_steps():

@@ -125,3 +125,53 @@ def test_config_field_offsets_match_header(tmp_path):
     got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
     assert got[:-1] == [getattr(_lib.Config, n).offset for n in names]
     assert got[-1] == ctypes.sizeof(_lib.Config)
+
+
+def _kernel_handles(path):
+    """Mangled names of the kernel handle symbols the library defines (nm; the device stubs excluded)."""
+    import shutil
+    import subprocess
+
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    out = subprocess.run([nm, "--defined-only", path], check=True, capture_output=True, text=True).stdout
+    return sorted(line.split()[-1] for line in out.splitlines()
+                  if line.split() and "__device_stub__" not in line and line.split()[-1].startswith("_ZN5tower"))
+
+
+def test_product_library_holds_only_the_shipped_trunk_kernels():
+    """The product build (make; no -DSPMCTS_AB) has one trunk kernel set per (board shape, channels,
+    dtype): 10 k_tower_dyn (device-count path: 7x6 and 3x3, C = 128 and 256, bf16 and fp16, + the
+    packed C = 256 one-buffer-tails set) and 14 k_tower (host-count path tiles), every Cfg without a
+    timing ablation (ABL = 0), the co-resident heads only, and no ring / LDS-heads / ablation kernel."""
+    path = _lib.LIB_PATH
+    if os.path.basename(path) != "libspmcts.so":
+        pytest.skip("SPMCTS_LIB points at another build")
+    names = _kernel_handles(path)
+    dyn = [n for n in names if n.startswith("_ZN5tower11k_tower_dyn")]
+    host = [n for n in names if n.startswith("_ZN5tower7k_tower")]
+    assert len(dyn) == 10 and len(host) == 14, (len(dyn), len(host))
+    # Cfg<C, ROWS, W, H, CG, WAVES, ABL, ...>: the 7th argument is 0 in every instantiation
+    cfgs = re.findall(r"(?:CfgI|NS1_I)Li(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E", " ".join(dyn + host))
+    assert cfgs and all(c[6] == "0" for c in cfgs)
+    assert {(c[0], c[2], c[3]) for c in cfgs} == {("128", "7", "6"), ("256", "7", "6"), ("128", "3", "3"),
+                                                 ("256", "3", "3")}
+    assert not [n for n in names if "ring" in n or n.startswith("_ZN5tower7k_headsI")]
+    assert len([n for n in names if n.startswith("_ZN5tower10k_heads_co")]) == 8
+
+
+def test_product_library_refuses_ab_switches(monkeypatch):
+    """An A/B-library switch in the environment is refused by the product library's tower entry
+    points (SPMCTS_ERR_AB_SWITCH = -5) before anything is launched, instead of being ignored."""
+    if os.path.basename(_lib.LIB_PATH) != "libspmcts.so":
+        pytest.skip("SPMCTS_LIB points at another build")
+    import subprocess
+    import sys
+
+    code = ("import ctypes, sys; sys.path.insert(0, %r); from self_play_reinforcement_learning_amd import _lib; "
+            "L = _lib.lib(); print(L.spmcts_tower_forward(7, 6, 128, 20, None, 0, None, None, None, 0, None))" % REPO)
+    env = dict(os.environ, SPMCTS_TOWER_CG="200")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True).stdout
+    assert out.split()[-1] == "-5"
+    env.pop("SPMCTS_TOWER_CG")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True).stdout
+    assert out.split()[-1] == "0"  # batch 0: nothing to do, no GPU call
