@@ -184,18 +184,31 @@ def cpu_baseline(seconds, cores, sims, filter_factor, num_blocks, threads=1, ope
     if os.path.exists(cal):
         with open(cal) as f:
             c = json.load(f)
-        # the reference's own pipeline over the port run the same way (random openings <-> bench mode)
+        # the reference's own pipeline over the port run the same way (random openings <-> bench mode), both
+        # on the build container's cores, back to back, as positions/s PER CORE: the reference used all
+        # c["cores"] cores (c["reference"]["play_workers"] play processes + its InferenceWorker), the port one
+        # process per core, so the ratio of per-core rates maps the port's per-core rate on this host to the
+        # reference's.  It applies to the same sims in flight per tree (the reference's thread_count).
         port = c["port_bench_mode"] if openings and "port_bench_mode" in c else c["port"]
-        r = c["reference"]["value"] / port["value"]
-        same = cores == c["cores"] and threads == c["reference"]["thread_count"]
-        out["calibration"] = dict(ratio_reference_over_port=r, source=os.path.relpath(cal, HERE),
-                                  calibrated_on=dict(cores=c["cores"], host=c.get("host"), port_sample=port["sample"]),
-                                  reference_equivalent=rate * r if same else None,
-                                  note=("the reference's own multiprocess pipeline vs this port, timed back to back on "
-                                        f"the build container's {c['cores']} cores; "
-                                        + ("reference_equivalent = value x ratio" if same else
-                                           f"not applied here ({cores} cores / {threads} sims in flight differ from "
-                                           "the calibration run; the ratio is from another host)")))
+        ref_pc = c["reference"]["value"] / c["reference"]["cores"]
+        port_pc = port["value"] / port["cores"]
+        r = ref_pc / port_pc
+        # the calibration ran the headline workload (200 sims, ResNet-128x20) at the reference's thread_count
+        same_k = threads == c["reference"]["thread_count"] and (sims, filter_factor, num_blocks) == (200, 32, 20)
+        out["calibration"] = dict(
+            ratio_reference_over_port_per_core=r, source=os.path.relpath(cal, HERE),
+            reference_per_core=ref_pc, port_per_core_calibration=port_pc, port_per_core_here=rate / cores,
+            calibrated_on=dict(cores=c["cores"], host=c.get("host"), port_sample=port["sample"],
+                               reference_sample=f"{c['reference']['play_workers']} play workers x "
+                                                f"{c['reference']['threads_per_worker']} game threads x "
+                                                f"thread_count {c['reference']['thread_count']} + InferenceWorker"),
+            reference_equivalent=rate * r if same_k else None,
+            reference_equivalent_per_core=rate / cores * r if same_k else None,
+            note=("reference_equivalent = value x the per-core ratio (the reference's multiprocess pipeline vs this "
+                  f"port, timed back to back on the build container's {c['cores']} cores), i.e. the reference's "
+                  f"pipeline on the {cores} cores used here at the same per-core scaling" if same_k else
+                  "not applied: the calibration ran 200 sims, ResNet-128x20, "
+                  f"{c['reference']['thread_count']} sims in flight per tree"))
     return out
 
 

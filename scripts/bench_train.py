@@ -3,9 +3,10 @@
 
 Workload: BASELINE configs[1] (Connect4, 200 sims, 4,096 games, ResNet-128x20, K = 4, two lanes) with
 the reference's trainer settings (batch 64, SGD lr 0.001 momentum 0.9 wd 1e-4, min_memory 20,000,
-memory 200,000).  The replay ring is first filled past min_memory (untimed), then --plies plies are
-timed with the trainer stepping, with its steps on their own stream (overlap, the default) or on the
-arena's stream, under fp16 autocast (the UpdateWorker's, the default) or in fp32, and once with
+memory 200,000).  `trainer_only`: ms per SGD step of the trainer alone (the update captured as one HIP
+graph, the default, or eager; fp16 autocast as the UpdateWorker, or fp32).  `runs`: the replay ring is
+first filled past min_memory (untimed), then --plies plies are timed with the trainer stepping (graphed
+steps on their own stream, the default; eager steps; steps on the arena's stream), and once with
 updates_per_ply = 0 for the self-play-only rate.
 
     python scripts/bench_train.py [--plies 24] [--updates 4]   -> one JSON line

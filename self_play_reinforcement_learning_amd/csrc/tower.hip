@@ -1031,8 +1031,8 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
     }
     const int wn_steps = L + 1 < n_convs ? LSTEPS : 0;
     if constexpr (K::XMAJ) {
-      static_assert((K::MG == 2 || (K::MG == 1 && K::EDGE)) &&
-                        (K::ABL & ~(2 | 4 | 8 | 16 | 128 | 512 | 4096 | 8192 | 16384)) == 0 && (K::ABL == 0 || K::EDGE),
+      static_assert(K::ONEBUF || ((K::MG == 2 || (K::MG == 1 && K::EDGE)) &&
+                        (K::ABL & ~(2 | 4 | 8 | 16 | 128 | 512 | 4096 | 8192 | 16384)) == 0 && (K::ABL == 0 || K::EDGE)),
                     "column-group conv: two row halves (edge tiles: or one); edge tiles take the 2/4/8/16/128 timing ablations");
       const bool even = (L & 1) == 0;
       if constexpr (K::MG == 1) {
@@ -1701,6 +1701,13 @@ static int forward_ab(int32_t width, int32_t height, int32_t channels, int32_t n
   }
   if (width == 7 && height == 6 && channels == 256 && cg == 254)  // the one-buffer trunk with a 4-deep weight ring
     return launch_split<Cfg<256, 256, 7, 6, 4, 4, 0, 4, 1, true, true, __bf16, true>, Cfg<256, 128, 7, 6, 4>,
+                        Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+  // the residual scratch through a buffer resource: nt policy (2561) / default policy (2562)
+  if (width == 7 && height == 6 && channels == 256 && cg == 2561)
+    return launch_split<Cfg<256, 256, 7, 6, 4, 4, 65536, 2, 1, true, true, __bf16, true>, Cfg<256, 128, 7, 6, 4>,
+                        Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+  if (width == 7 && height == 6 && channels == 256 && cg == 2562)
+    return launch_split<Cfg<256, 256, 7, 6, 4, 4, 131072, 2, 1, true, true, __bf16, true>, Cfg<256, 128, 7, 6, 4>,
                         Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
   return 1;
 }

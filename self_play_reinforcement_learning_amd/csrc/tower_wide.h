@@ -36,6 +36,31 @@ struct Scr {
 };
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+// Residual-scratch access through a buffer resource over this workgroup's region (Cfg ABL bit 65536 =
+// nt cache policy, as the pointer form's nontemporal accesses; 131072 = default policy, an A/B probe of
+// the vector-L1 question): the per-lane part is one 32-bit voffset (lane * 32 + half * 16) and the
+// (wave, channel tile, cell tile) part a wave-uniform soffset, instead of 16 hoisted 64-bit addresses.
+template <class K>
+struct ScrBuf {
+  static constexpr int AUX = (K::ABL & 65536) ? 2 : 0;  // gfx950 CPol: nt = 2
+  __amdgpu_buffer_rsrc_t rsrc;
+  __device__ __forceinline__ explicit ScrBuf(uint4 *base) {
+    rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)Scr<K>::PER_WG, 0x00020000);
+  }
+  __device__ static __forceinline__ int soff(int wave, int m, int t) {
+    return (int)(((size_t)wave * K::MT + m) * K::NT + t) * 64 * 32;
+  }
+  __device__ __forceinline__ uint4 load(int lane, int half, int so) const {
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane * 32 + half * 16, so, AUX));
+  }
+  __device__ __forceinline__ void store(uint4 v, int lane, int half, int so) const {
+    typedef int i32x4 __attribute__((ext_vector_type(4)));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rsrc, lane * 32 + half * 16, so, AUX);
+  }
+};
+template <class K>
+constexpr bool kScrRsrc = (K::ABL & (65536 | 131072)) != 0;
+
 // In-place epilogue of a conv (or the stem): every wave has finished reading the buffer (barrier
 // before), out = relu(acc + bias (+ residual from scratch)) into the lane's own rows; SAVE also stores
 // the outputs to scratch (the next block's residual).  A barrier publishes the outputs.
@@ -54,10 +79,17 @@ __device__ __forceinline__ void epilogue(char *X, const f32x16 (&acc)[K::MT][K::
     if constexpr (RESID) {
 #pragma unroll
       for (int i = 0; i < HT; ++i) {
-        // nontemporal (nt): served from L2, never from a vector-L1 line an earlier read left behind
-        const u32x4 *p = (const u32x4 *)Scr<K>::at(scr, wave, m, t0 + i, lane);
-        res[i][0] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(p));
-        res[i][1] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(p + 1));
+        if constexpr (kScrRsrc<K>) {
+          const ScrBuf<K> sb(scr);
+          const int so = ScrBuf<K>::soff(__builtin_amdgcn_readfirstlane(wave), m, t0 + i);
+          res[i][0] = sb.load(lane, 0, so);
+          res[i][1] = sb.load(lane, 1, so);
+        } else {
+          // nontemporal (nt): served from L2, never from a vector-L1 line an earlier read left behind
+          const u32x4 *p = (const u32x4 *)Scr<K>::at(scr, wave, m, t0 + i, lane);
+          res[i][0] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(p));
+          res[i][1] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(p + 1));
+        }
       }
     }
 #pragma unroll
@@ -83,7 +115,12 @@ __device__ __forceinline__ void epilogue(char *X, const f32x16 (&acc)[K::MT][K::
       const uint4 lo = make_uint4(o[0], o[1], o[2], o[3]), hi = make_uint4(o[4], o[5], o[6], o[7]);
       *(uint4 *)p = lo;
       *(uint4 *)(p + 16) = hi;
-      if constexpr (SAVE) {
+      if constexpr (SAVE && kScrRsrc<K>) {
+        const ScrBuf<K> sb(scr);
+        const int so = ScrBuf<K>::soff(__builtin_amdgcn_readfirstlane(wave), m, t);
+        sb.store(lo, lane, 0, so);
+        sb.store(hi, lane, 1, so);
+      } else if constexpr (SAVE) {
         u32x4 *q = (u32x4 *)Scr<K>::at(scr, wave, m, t, lane);
         __builtin_nontemporal_store(__builtin_bit_cast(u32x4, lo), q);
         __builtin_nontemporal_store(__builtin_bit_cast(u32x4, hi), q + 1);

@@ -693,3 +693,8 @@ def test_bench_line_small_with_no_dedup_twin():
     assert 0 < d["roofline"]["frac"] < 1 and d["config"]["leaf_dedup"] is True and d["nn"]["rows_per_leaf"] <= 1.0
     tw = d["no_dedup_twin"]
     assert tw["plies"] == 2 and tw["value"] > 0 and tw["rows_per_leaf"] == 1.0
+    # the default dtype is the reference's fp16; the bf16 trunk is timed on the same games afterwards
+    assert d["dtype"] == "fp16" and d["secondary_dtype"]["dtype"] == "bf16" and d["secondary_dtype"]["value"] > 0
+    r = d["ranks"]
+    assert r["world_size"] == 1 and len(r["per_rank"]) == 1
+    assert r["positions_per_s_min"] == r["positions_per_s_max"] == r["per_rank"][0]["positions_per_s"]
