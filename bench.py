@@ -246,9 +246,9 @@ def main():
     ap.add_argument("--dtype", choices=["bf16", "fp16"], default="fp16",
                     help="element type of the fused trunk's weights / activations (fp32 accumulation); fp16 (the "
                          "default) is the reference's own inference dtype (amp.autocast, inference_worker.py:117)")
-    ap.add_argument("--secondary-plies", type=int, default=5, metavar="PLIES",
-                    help="after the timed region (and the no-dedup twin), time PLIES more plies of the same games "
-                         "with the other trunk dtype (bf16 <-> fp16): reported as secondary_dtype")
+    ap.add_argument("--no-secondary", dest="secondary", action="store_false",
+                    help="skip the secondary line: the other trunk dtype (bf16 <-> fp16) on a fresh engine with the "
+                         "same seeds, --warmup and --steps, reported as secondary_dtype")
     ap.add_argument("--search-threads", type=int, default=4,
                     help="sims in flight per tree with virtual loss: the reference's thread_count search "
                          "(mcts.py:328-331), 4 in its headline self-play setup (InferenceProxy workers, "
@@ -549,37 +549,63 @@ def main():
             "rows_per_leaf": (t_c1["nn_rows"] - t_c0["nn_rows"]) / max(1, t_c1["nn_leaves"] - t_c0["nn_leaves"]),
             "note": "the plies right after the timed region, leaf dedup off (spmcts_set_leaf_dedup): every leaf "
                     "evaluated in its own row, as the reference's InferenceWorker"}
-    if args.secondary_plies > 0 and not arena_mode:
-        # the same games with the trunk in the other element type (a secondary figure; `value` is the
-        # --dtype line): every lane's fused evaluator repacks its weights (HipTowerEvaluator.set_dtype)
+    if args.secondary and not arena_mode:
+        # the other trunk element type (bf16 <-> fp16) on a FRESH engine with the same seeds, warm-up and
+        # timed plies as the headline (games of the same age, so the two lines compare like for like);
+        # `value` is the --dtype line.  The headline arenas are released first.
         other = {"bf16": "fp16", "fp16": "bf16"}[args.dtype]
-        evs = [e.evaluator for e in getattr(eng, "lanes", [eng])]
-        if all(hasattr(ev, "set_dtype") for ev in evs):
-            for ev in evs:
-                ev.set_dtype({"bf16": torch.bfloat16, "fp16": torch.float16}[other])
-            eng.refresh_network()
-            eng.check()
-            s_c0 = eng.counters()
-            D.barrier()
-            torch.cuda.synchronize()
-            s_t0 = time.perf_counter()
-            for _ in range(args.secondary_plies):
-                one_step()
-            if D.is_distributed() and args.secondary_plies % args.exchange_every:
-                ex.end_ply(eng.stats_vector, force=True)
-            D.barrier()
-            torch.cuda.synchronize()
-            s_el = D.all_reduce_max(time.perf_counter() - s_t0)
-            s_c1 = eng.counters()
-            eng.check()
-            s_moves = int(D.all_reduce_stats([s_c1["moves"] - s_c0["moves"]])[0])
-            out["secondary_dtype"] = {
-                "dtype": other, "plies": args.secondary_plies, "value": s_moves / s_el,
-                "ms_per_step": s_el / args.secondary_plies * 1e3,
-                "leaf_dedup": bool(getattr(eng, "leaf_dedup", False)),
-                "rows_per_leaf": (s_c1["nn_rows"] - s_c0["nn_rows"]) / max(1, s_c1["nn_leaves"] - s_c0["nn_leaves"]),
-                "note": f"the plies after the timed region{' and the no-dedup twin' if 'no_dedup_twin' in out else ''}, "
-                        f"the fused trunk and heads repacked in {other}"}
+        for e in getattr(eng, "lanes", [eng]):
+            e.arena.close()
+        del eng
+        torch.cuda.empty_cache()
+        kw2 = dict(kw, dtype={"bf16": torch.bfloat16, "fp16": torch.float16}[other])
+        if args.lanes > 1:
+            eng2 = LanedEngine("connect4", net, n_games=args.games, lanes=args.lanes, pack=not args.no_pack, **kw2)
+        else:
+            eng2 = SelfPlayEngine("connect4", net, n_games=args.games, **kw2)
+        ex2 = D.MoveExchange(42, 7, sink=lambda g: None, every=args.exchange_every)
+
+        def step2():
+            eng2.ply(on_moves=ex2.stage if not args.no_gather else None)
+            ex2.end_ply(eng2.stats_vector if D.is_distributed() else None)
+
+        for _ in range(args.warmup):
+            step2()
+        if D.is_distributed() and args.warmup % args.exchange_every:
+            ex2.end_ply(eng2.stats_vector, force=True)
+        eng2.check()
+        s_c0 = eng2.counters()
+        eng2.enable_timers(True)
+        D.barrier()
+        torch.cuda.synchronize()
+        ref2 = torch.cuda.Event(enable_timing=True)
+        ref2.record()
+        s_t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step2()
+        if D.is_distributed() and args.steps % args.exchange_every:
+            ex2.end_ply(eng2.stats_vector, force=True)
+        D.barrier()
+        torch.cuda.synchronize()
+        s_el = D.all_reduce_max(time.perf_counter() - s_t0)
+        s_c1 = eng2.counters()
+        eng2.check()
+        s_moves = int(D.all_reduce_stats([s_c1["moves"] - s_c0["moves"]])[0])
+        s_rows = s_c1["nn_rows"] - s_c0["nn_rows"]
+        t2 = eng2.tower_timer
+        s_launches = max(1, t2.count() // lanes)
+        s_tw_s = union_ms(t2.intervals(ref2)) / 1e3 / s_launches
+        s_tflops = s_rows * trunk_fpl / s_launches / s_tw_s / 1e12 if s_tw_s > 0 else 0.0
+        out["secondary_dtype"] = {
+            "dtype": other, "value": s_moves / s_el, "unit": "positions/s", "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": s_el / args.steps * 1e3,
+            "rows_per_leaf": s_rows / max(1, s_c1["nn_leaves"] - s_c0["nn_leaves"]),
+            "roofline": {"achieved": s_tflops, "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": s_tflops / BF16_DENSE_PEAK_TFLOPS, "avg_launch_us": s_tw_s * 1e6},
+            "note": f"a fresh engine with the same seeds, warm-up and timed plies as the headline, the fused trunk "
+                    f"and heads in {other}; the headline `value` is --dtype {args.dtype}"}
+        for e in getattr(eng2, "lanes", [eng2]):
+            e.arena.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if D.is_distributed():
