@@ -43,8 +43,24 @@ def main(path, plies=7, lanes=2):
             o = min(b, e) - max(a, s)
             if o > 0:
                 att[n] += o
+    # windows by ply phase: one holding a k_select_vl (the first fill of a ply's searches), one holding
+    # the ply-end kernels (move choice, finish / refill), or a simulation step's window (expand / leaf rows)
+    cls = collections.Counter()
+    ncls = collections.Counter()
+    durs = []
+    for a, b in free:
+        names = {n for s, e, n in sub if min(b, e) - max(a, s) > 0}
+        k = ("ply_start" if any("k_select_vl" in n for n in names) else
+             "ply_end" if any("k_games" in n for n in names) else "sim_step")
+        cls[k] += b - a
+        ncls[k] += 1
+        durs.append((b - a) / 1e3)
+    durs.sort()
+    q = lambda f: durs[min(len(durs) - 1, int(f * len(durs)))] if durs else 0.0
     res = dict(span_ms=span / 1e6, idle_frac=1 - sum(e - s for s, e in busy) / span,
                tower_free_frac=sum(b - a for a, b in free) / span, tower_free_windows=len(free),
+               window_us_quantiles={"p10": q(0.1), "p50": q(0.5), "p90": q(0.9), "max": q(1.0)},
+               by_phase_frac={k: v / span for k, v in cls.items()}, by_phase_windows=dict(ncls),
                overlapping_kernels_ms={k: v / 1e6 for k, v in att.most_common(8)})
     print(json.dumps(res, indent=1))
 

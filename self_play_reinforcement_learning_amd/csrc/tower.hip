@@ -1709,6 +1709,16 @@ static int forward_ab(int32_t width, int32_t height, int32_t channels, int32_t n
   if (width == 7 && height == 6 && channels == 256 && cg == 2562)
     return launch_split<Cfg<256, 256, 7, 6, 4, 4, 131072, 2, 1, true, true, __bf16, true>, Cfg<256, 128, 7, 6, 4>,
                         Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+  // probes: rsrc loads + pointer stores (2563), pointer loads + rsrc stores (2564), both rsrc with sc0 sc1 (2565)
+  if (width == 7 && height == 6 && channels == 256 && cg == 2563)
+    return launch_split<Cfg<256, 256, 7, 6, 4, 4, 262144, 2, 1, true, true, __bf16, true>, Cfg<256, 128, 7, 6, 4>,
+                        Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+  if (width == 7 && height == 6 && channels == 256 && cg == 2564)
+    return launch_split<Cfg<256, 256, 7, 6, 4, 4, 524288, 2, 1, true, true, __bf16, true>, Cfg<256, 128, 7, 6, 4>,
+                        Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+  if (width == 7 && height == 6 && channels == 256 && cg == 2565)
+    return launch_split<Cfg<256, 256, 7, 6, 4, 4, 1048576, 2, 1, true, true, __bf16, true>, Cfg<256, 128, 7, 6, 4>,
+                        Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
   return 1;
 }
 }  // namespace tower

@@ -42,7 +42,8 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // (wave, channel tile, cell tile) part a wave-uniform soffset, instead of 16 hoisted 64-bit addresses.
 template <class K>
 struct ScrBuf {
-  static constexpr int AUX = (K::ABL & 65536) ? 2 : 0;  // gfx950 CPol: nt = 2
+  // gfx950 CPol: nt = 2, sc0 = 1, sc1 = 16
+  static constexpr int AUX = (K::ABL & (65536 | 262144 | 524288)) ? 2 : (K::ABL & 1048576) ? 17 : 0;
   __amdgpu_buffer_rsrc_t rsrc;
   __device__ __forceinline__ explicit ScrBuf(uint4 *base) {
     rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)Scr<K>::PER_WG, 0x00020000);
@@ -58,8 +59,12 @@ struct ScrBuf {
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rsrc, lane * 32 + half * 16, so, AUX);
   }
 };
+// which residual-scratch accesses go through the buffer resource (A/B probes of the round-3 finding that
+// the rsrc form gives different outputs): 262144 = loads only, 524288 = stores only, 1048576 = both (sc0 sc1)
 template <class K>
-constexpr bool kScrRsrc = (K::ABL & (65536 | 131072)) != 0;
+constexpr bool kScrRsrcLd = (K::ABL & (65536 | 131072 | 262144 | 1048576)) != 0;
+template <class K>
+constexpr bool kScrRsrcSt = (K::ABL & (65536 | 131072 | 524288 | 1048576)) != 0;
 
 // In-place epilogue of a conv (or the stem): every wave has finished reading the buffer (barrier
 // before), out = relu(acc + bias (+ residual from scratch)) into the lane's own rows; SAVE also stores
@@ -79,7 +84,7 @@ __device__ __forceinline__ void epilogue(char *X, const f32x16 (&acc)[K::MT][K::
     if constexpr (RESID) {
 #pragma unroll
       for (int i = 0; i < HT; ++i) {
-        if constexpr (kScrRsrc<K>) {
+        if constexpr (kScrRsrcLd<K>) {
           const ScrBuf<K> sb(scr);
           const int so = ScrBuf<K>::soff(__builtin_amdgcn_readfirstlane(wave), m, t0 + i);
           res[i][0] = sb.load(lane, 0, so);
@@ -115,7 +120,7 @@ __device__ __forceinline__ void epilogue(char *X, const f32x16 (&acc)[K::MT][K::
       const uint4 lo = make_uint4(o[0], o[1], o[2], o[3]), hi = make_uint4(o[4], o[5], o[6], o[7]);
       *(uint4 *)p = lo;
       *(uint4 *)(p + 16) = hi;
-      if constexpr (SAVE && kScrRsrc<K>) {
+      if constexpr (SAVE && kScrRsrcSt<K>) {
         const ScrBuf<K> sb(scr);
         const int so = ScrBuf<K>::soff(__builtin_amdgcn_readfirstlane(wave), m, t);
         sb.store(lo, lane, 0, so);

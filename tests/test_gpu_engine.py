@@ -200,6 +200,7 @@ def test_trainer_graph_matches_eager_steps(autocast):
     for graph in (False, True):
         torch.manual_seed(0)
         net = ResidualTower(7, 6, 7, num_blocks=2, filter_factor=16).cuda()
+        w_init = {k: v.clone() for k, v in net.state_dict().items()}
         opt = torch.optim.SGD(net.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
         tr = _Trainer(net, opt, memory_size=1000, batch_size=64, min_memory=0, q_average=True, device="cuda",
                       overlap=False, autocast=autocast, train_mode=False, graph=graph)
@@ -219,8 +220,21 @@ def test_trainer_graph_matches_eager_steps(autocast):
     (w0, l0), (w1, l1) = out
     assert all(math.isfinite(x) for x in l1)
     assert max(abs(a - b) for a, b in zip(l0, l1)) < 1e-4 * max(abs(x) for x in l0), (l0, l1)
+    # the replayed kernels need not be the eager ones bit for bit (MIOpen may pick another algorithm under
+    # capture, and its fp16 kernels round differently): each tensor's total update over the 10 steps must
+    # agree to 1e-3 of its norm in fp32 and to 5e-2 under fp16 autocast (one step lost or repeated would
+    # move it by ~1e-1)
+    tol = 5e-2 if autocast else 1e-3
+    rel = {}
     for k in w0:
-        torch.testing.assert_close(w0[k], w1[k], rtol=1e-4, atol=1e-6, msg=k)
+        if not w0[k].is_floating_point():
+            assert torch.equal(w0[k], w1[k]), k
+            continue
+        d0, d1 = (w0[k] - w_init[k]).double(), (w1[k] - w_init[k]).double()
+        rel[k] = (d0 - d1).norm().item() / (d0.norm().item() + 1e-12)
+    print("graph vs eager, update rel. difference: max", max(rel.values()), "median", sorted(rel.values())[len(rel) // 2])
+    bad = {k: r for k, r in rel.items() if r > tol}
+    assert not bad, bad
 
 
 def test_trainer_graph_train_mode_replays_run():

@@ -374,19 +374,29 @@ def test_evaluation_games_per_side_threads_match_oracle(key, k0, k1):
             assert float(q) == float(M["q"]), (gi, i)
 
 
+_TREE_BLOCK_CHILD = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+from tests.parity_helpers import g2_threaded, run_g2_group
+from tests.test_gpu_parity import _threaded_groups
+key, cases = _threaded_groups()[0]
+runs = [g2_threaded(c, 4) for c in cases]
+res, counters = run_g2_group(cases, search_threads=4, tapes=[t for t, _ in runs])
+assert counters["error_flags"] == 0
+for c, (_, e), r in zip(cases, runs, res):
+    assert r["child_n"] == e["child_n"] and r["child_w"] == e["child_w"], c["id"]
+    assert r["action"] == e["action"], c["id"]
+print("ok", len(cases))
+"""
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("tree_block", [512, 8])
-def test_threaded_search_tree_workgroups(tree_block, monkeypatch):
+def test_threaded_search_tree_workgroups(tree_block):
     """The threaded tree kernels give the same searches with 8 trees per 64-thread workgroup (the
-    default), 64 trees per 512-thread workgroup, or one tree per workgroup (SPMCTS_TREE_BLOCK, read
-    when an arena is created)."""
-    from tests.parity_helpers import g2_threaded
+    default), 64 trees per 512-thread workgroup, or one tree per workgroup (the A/B library's
+    SPMCTS_TREE_BLOCK, read when an arena is created; run in a child process on that library)."""
+    from tests.ab_lib import ab_env, run_child
 
-    monkeypatch.setenv("SPMCTS_TREE_BLOCK", str(tree_block))
-    key, cases = _threaded_groups()[0]
-    runs = [g2_threaded(c, 4) for c in cases]
-    res, counters = run_g2_group(cases, search_threads=4, tapes=[t for t, _ in runs])
-    assert counters["error_flags"] == 0
-    for c, (_, e), r in zip(cases, runs, res):
-        assert r["child_n"] == e["child_n"] and r["child_w"] == e["child_w"], c["id"]
-        assert r["action"] == e["action"], c["id"]
+    out = run_child(_TREE_BLOCK_CHILD, ab_env(SPMCTS_TREE_BLOCK=tree_block))
+    assert out.split()[-2] == "ok", out

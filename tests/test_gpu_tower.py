@@ -146,29 +146,42 @@ def test_zero_and_maximum_rows():
     assert torch.equal(probs[:64], ref_p) and torch.equal(values[:64].view(-1), ref_v.view(-1))
 
 
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("game,n,ff", [("connect4", 1, 32), ("connect4", 31, 32), ("connect4", 33, 32),
-                                       ("connect4", 1000, 32), ("connect4", 4096, 32), ("tictactoe", 77, 32),
-                                       ("connect4", 33, 64), ("connect4", 1000, 64), ("tictactoe", 77, 64)])
-def test_coresident_heads_match_lds_heads(game, n, ff, dtype, monkeypatch):
-    """k_heads_co (features read from global memory, 32 boards per workgroup, 96 registers: fits beside
-    a trunk workgroup; C = 256: two value passes in 72 registers) gives the LDS-staged k_heads' results
-    bit for bit: same per-wave k order, same fixed-order cross-wave sums; ragged tails (n % 32) read
-    only live boards."""
-    W, H, A = (7, 6, 7) if game == "connect4" else (3, 3, 9)
-    net = _net(W, H, A, 2, ff)
-    x = _planes(W, H, n, seed=11).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    hip = HipTowerEvaluator(net, dtype=dtype)
-    monkeypatch.setenv("SPMCTS_HEADS", "lds")
-    monkeypatch.setenv("SPMCTS_HEADS_C256", "lds")
-    p0, v0 = hip(x)
-    torch.cuda.synchronize()
-    monkeypatch.delenv("SPMCTS_HEADS")
-    monkeypatch.delenv("SPMCTS_HEADS_C256")
-    p1, v1 = hip(x)
-    torch.cuda.synchronize()
-    assert torch.equal(p0, p1) and torch.equal(v0, v1)
-    assert torch.isfinite(p1).all() and torch.isfinite(v1).all()
+_HEADS_CASES = [("connect4", 1, 32), ("connect4", 31, 32), ("connect4", 33, 32), ("connect4", 1000, 32),
+                ("connect4", 4096, 32), ("tictactoe", 77, 32), ("connect4", 33, 64), ("connect4", 1000, 64),
+                ("tictactoe", 77, 64)]
+
+_HEADS_CHILD = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+from tests.test_gpu_tower import _net, _planes, _HEADS_CASES
+from self_play_reinforcement_learning_amd.evaluator import HipTowerEvaluator
+out = {}
+for dt, name in ((torch.bfloat16, "bf16"), (torch.float16, "fp16")):
+    for game, n, ff in _HEADS_CASES:
+        W, H, A = (7, 6, 7) if game == "connect4" else (3, 3, 9)
+        x = _planes(W, H, n, seed=11).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        p, v = HipTowerEvaluator(_net(W, H, A, 2, ff), dtype=dt)(x)
+        key = f"{name}_{game}_{n}_{ff}"
+        out["p_" + key], out["v_" + key] = p.float().cpu().numpy(), v.float().cpu().numpy()
+np.savez(sys.argv[2], **out)
+"""
+
+
+def test_coresident_heads_match_lds_heads(tmp_path):
+    """k_heads_co (the product library's heads: features read from global memory, 32 boards per workgroup,
+    96 registers, so it fits beside a trunk workgroup; C = 256: two value passes) gives the LDS-staged k_heads'
+    results (the A/B library's SPMCTS_HEADS=lds / SPMCTS_HEADS_C256=lds, in a child process) bit for bit: same
+    per-wave k order, same fixed-order cross-wave sums; ragged tails (n % 32) read only live boards; bf16 and
+    fp16, C = 128 and 256."""
+    from tests.ab_lib import ab_env, product_env, run_child
+
+    run_child(_HEADS_CHILD, ab_env(SPMCTS_HEADS="lds", SPMCTS_HEADS_C256="lds"), tmp_path / "lds.npz")
+    run_child(_HEADS_CHILD, product_env(), tmp_path / "co.npz")
+    lds, co = np.load(tmp_path / "lds.npz"), np.load(tmp_path / "co.npz")
+    assert sorted(lds.files) == sorted(co.files) and len(co.files) == 4 * len(_HEADS_CASES)
+    for k in co.files:
+        assert np.array_equal(lds[k], co[k]), k
+        assert np.isfinite(co[k]).all(), k
 
 
 @pytest.mark.parametrize("ff", [32, 64])
@@ -226,8 +239,10 @@ def test_ring_trunk_variant():
     import subprocess
     import sys
 
+    from tests.ab_lib import ab_env
+
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, SPMCTS_TOWER_RING="1")
+    env = ab_env(SPMCTS_TOWER_RING="1")  # the ring trunk is in the A/B library only
     r = subprocess.run([sys.executable, "-c", _RING_CHILD.format(repo=repo)], env=env, capture_output=True, text=True,
                        timeout=240, cwd=repo)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -255,17 +270,20 @@ np.savez(sys.argv[2], **out)
 
 
 def test_wide_c256_tiles_bit_identical(tmp_path):
-    """The one-buffer 6-board C = 256 trunk (tower_wide.h, SPMCTS_TOWER_C256=6, read once per process)
-    gives every board the same bits as the default 3-board tiles: host batch (full tiles + tails) and
+    """The one-buffer 6-board C = 256 trunk (tower_wide.h, the product library's default) gives every board
+    the same bits as the 3-board tiles (the A/B library's SPMCTS_TOWER_C256=3, read once per process): host batch (full tiles + tails) and
     the device-count path on a ragged batch, bf16 and fp16."""
     import os
     import subprocess
     import sys
 
+    from tests.ab_lib import ab_env, product_env
+
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     res = {}
     for tiles in ("3", "6"):
-        env = dict(os.environ, SPMCTS_TOWER_C256=tiles)
+        # the 3-board tiles are an A/B-library alternate; the 6-board tiles are the product library's trunk
+        env = ab_env(SPMCTS_TOWER_C256="3") if tiles == "3" else product_env()
         out = tmp_path / f"c{tiles}.npz"
         subprocess.run([sys.executable, "-c", _WIDE_CHILD, root, str(out)], env=env, check=True, timeout=300)
         res[tiles] = np.load(out)
