@@ -236,6 +236,9 @@ def main():
                     help="arenas per GPU on their own HIP streams (engine.LanedEngine); 1 = one arena")
     ap.add_argument("--blocks-per-tree", type=int, default=0,
                     help="node blocks per tree; below the worst case the arena recycles subtrees (k_compact)")
+    ap.add_argument("--no-stagger", action="store_true",
+                    help="lanes in lock step (every lane's ply boundary at the same time) instead of lane i "
+                         "i * S / lanes simulation steps behind lane 0 (engine.LanedEngine stagger)")
     ap.add_argument("--no-pack", action="store_true",
                     help="lanes > 1: keep round-aligned tower tiles (no SPMCTS_TOWER_PACK)")
     ap.add_argument("--twin-no-dedup", type=int, default=5, metavar="PLIES",
@@ -300,7 +303,8 @@ def main():
               evaluate=arena_mode, record=not arena_mode, search_threads=args.search_threads,
               blocks_per_tree=args.blocks_per_tree, leaf_dedup=False if args.no_leaf_dedup else None)
     if args.lanes > 1:
-        eng = LanedEngine("connect4", net, n_games=args.games, lanes=args.lanes, pack=not args.no_pack, **kw)
+        eng = LanedEngine("connect4", net, n_games=args.games, lanes=args.lanes, pack=not args.no_pack,
+                          stagger=not args.no_stagger, **kw)
     else:
         eng = SelfPlayEngine("connect4", net, n_games=args.games, **kw)
     gathered = []
@@ -434,6 +438,7 @@ def main():
             "net": f"ResidualTower(filter_factor={args.filter_factor}, num_blocks={args.blocks})",
             "parallelism": f"dp{world}",
             "lanes_per_gpu": max(1, args.lanes),
+            "lanes_staggered": bool(getattr(eng, "stagger", False)) if args.lanes > 1 else False,
             "search_threads": args.search_threads,
             "leaf_dedup": bool(getattr(eng, "leaf_dedup", False)),
         },
@@ -560,7 +565,8 @@ def main():
         torch.cuda.empty_cache()
         kw2 = dict(kw, dtype={"bf16": torch.bfloat16, "fp16": torch.float16}[other])
         if args.lanes > 1:
-            eng2 = LanedEngine("connect4", net, n_games=args.games, lanes=args.lanes, pack=not args.no_pack, **kw2)
+            eng2 = LanedEngine("connect4", net, n_games=args.games, lanes=args.lanes, pack=not args.no_pack,
+                               stagger=not args.no_stagger, **kw2)
         else:
             eng2 = SelfPlayEngine("connect4", net, n_games=args.games, **kw2)
         ex2 = D.MoveExchange(42, 7, sink=lambda g: None, every=args.exchange_every)

@@ -4,7 +4,7 @@
 set -u
 mkdir -p gpurun_out/prof
 export TMPDIR=/tmp
-ARGS="--steps ${PSTEPS:-3} --warmup ${PWARM:-24} --no-cpu-baseline --lanes ${LANES:-2} --twin-no-dedup 0 --secondary-plies 0 ${EXTRA:-}"
+ARGS="--steps ${PSTEPS:-3} --warmup ${PWARM:-24} --no-cpu-baseline --lanes ${LANES:-2} --twin-no-dedup 0 --no-secondary ${EXTRA:-}"
 # the timed region's dispatch count of a bench JSON line (the reducers keep only those)
 ndisp() { python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][0]); print(d[sys.argv[2]][sys.argv[3]])" "$@"; }
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof/trace -o run -- \

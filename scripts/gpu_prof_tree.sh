@@ -3,7 +3,7 @@
 set -u
 mkdir -p gpurun_out/tree
 export TMPDIR=/tmp
-ARGS="--steps ${PSTEPS:-3} --warmup ${PWARM:-24} --no-cpu-baseline --twin-no-dedup 0 --secondary-plies 0 ${EXTRA:-}"
+ARGS="--steps ${PSTEPS:-3} --warmup ${PWARM:-24} --no-cpu-baseline --twin-no-dedup 0 --no-secondary ${EXTRA:-}"
 ndisp() { python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][0]); print(d[sys.argv[2]][sys.argv[3]])" "$@"; }
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/tree/trace -o run -- \
   python3 bench.py $ARGS > gpurun_out/tree/bench_traced.json 2> gpurun_out/tree/trace.err

@@ -1702,22 +1702,10 @@ static int forward_ab(int32_t width, int32_t height, int32_t channels, int32_t n
   if (width == 7 && height == 6 && channels == 256 && cg == 254)  // the one-buffer trunk with a 4-deep weight ring
     return launch_split<Cfg<256, 256, 7, 6, 4, 4, 0, 4, 1, true, true, __bf16, true>, Cfg<256, 128, 7, 6, 4>,
                         Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-  // the residual scratch through a buffer resource: nt policy (2561) / default policy (2562)
-  if (width == 7 && height == 6 && channels == 256 && cg == 2561)
-    return launch_split<Cfg<256, 256, 7, 6, 4, 4, 65536, 2, 1, true, true, __bf16, true>, Cfg<256, 128, 7, 6, 4>,
-                        Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-  if (width == 7 && height == 6 && channels == 256 && cg == 2562)
-    return launch_split<Cfg<256, 256, 7, 6, 4, 4, 131072, 2, 1, true, true, __bf16, true>, Cfg<256, 128, 7, 6, 4>,
-                        Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-  // probes: rsrc loads + pointer stores (2563), pointer loads + rsrc stores (2564), both rsrc with sc0 sc1 (2565)
-  if (width == 7 && height == 6 && channels == 256 && cg == 2563)
-    return launch_split<Cfg<256, 256, 7, 6, 4, 4, 262144, 2, 1, true, true, __bf16, true>, Cfg<256, 128, 7, 6, 4>,
-                        Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-  if (width == 7 && height == 6 && channels == 256 && cg == 2564)
-    return launch_split<Cfg<256, 256, 7, 6, 4, 4, 524288, 2, 1, true, true, __bf16, true>, Cfg<256, 128, 7, 6, 4>,
-                        Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
-  if (width == 7 && height == 6 && channels == 256 && cg == 2565)
-    return launch_split<Cfg<256, 256, 7, 6, 4, 4, 1048576, 2, 1, true, true, __bf16, true>, Cfg<256, 128, 7, 6, 4>,
+  // the round-3 residual-scratch pointer form (64-bit nontemporal accesses, 110 spills) against the shipped
+  // buffer-resource form (tower_wide.h ScrBuf)
+  if (width == 7 && height == 6 && channels == 256 && cg == 2566)
+    return launch_split<Cfg<256, 256, 7, 6, 4, 4, 2097152, 2, 1, true, true, __bf16, true>, Cfg<256, 128, 7, 6, 4>,
                         Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
   return 1;
 }
@@ -1756,9 +1744,11 @@ extern "C" int spmcts_tower_forward(int32_t width, int32_t height, int32_t chann
   const char *pl = (const char *)planes_dev;
   char *ft = (char *)features_dev;
 #ifdef SPMCTS_AB
+  // the ring trunk serves both element types on both paths (as spmcts_tower_forward_dev)
+  if (width == 7 && height == 6 && channels == 128 && ring_enabled(n_blocks) && !getenv("SPMCTS_TOWER_CG"))
+    return (flags & SPMCTS_TOWER_F16 ? launch_ring<_Float16> : launch_ring<__bf16>)(
+        planes_dev, nullptr, batch, n_blocks, weights_dev, bias_dev, features_dev, s);
   if (!(flags & SPMCTS_TOWER_F16)) {
-    if (width == 7 && height == 6 && channels == 128 && ring_enabled(n_blocks) && !getenv("SPMCTS_TOWER_CG"))
-      return launch_ring<__bf16>(planes_dev, nullptr, batch, n_blocks, weights_dev, bias_dev, features_dev, s);
     const int rc = forward_ab(width, height, channels, n_blocks, pl, batch, weights_dev, bias_dev, ft, s);
     if (rc != 1) return rc;
   }

@@ -36,14 +36,18 @@ struct Scr {
 };
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-// Residual-scratch access through a buffer resource over this workgroup's region (Cfg ABL bit 65536 =
-// nt cache policy, as the pointer form's nontemporal accesses; 131072 = default policy, an A/B probe of
-// the vector-L1 question): the per-lane part is one 32-bit voffset (lane * 32 + half * 16) and the
-// (wave, channel tile, cell tile) part a wave-uniform soffset, instead of 16 hoisted 64-bit addresses.
+// Residual-scratch access through a buffer resource over this workgroup's region: the per-lane part of a
+// load's address is one 32-bit voffset (lane * 32 + half * 16) and the (wave, channel tile, cell tile) part a
+// wave-uniform soffset, instead of 16 hoisted 64-bit addresses (the pointer form spilled 110 VGPRs on them).
+// Stores take the whole offset in the voffset and soffset = 0: hipcc (ROCm 7.2) inserts no wait state between
+// a buffer_store_dwordx4 whose soffset is an SGPR and a following VALU write of its data VGPRs (LLVM's
+// store-data hazard check exempts a register soffset), and on gfx950 that form stored wrong data -- every
+// C = 256 output differed (profiles/r04/c256_rsrc/probe_summary.txt: rsrc loads + pointer stores bit-equal,
+// pointer loads + SGPR-soffset rsrc stores not).  With soffset = 0 the hazard check applies.
+// A/B library: Cfg ABL bit 2097152 = the round-3 pointer form (nontemporal 64-bit accesses).
 template <class K>
 struct ScrBuf {
-  // gfx950 CPol: nt = 2, sc0 = 1, sc1 = 16
-  static constexpr int AUX = (K::ABL & (65536 | 262144 | 524288)) ? 2 : (K::ABL & 1048576) ? 17 : 0;
+  static constexpr int AUX = 2;  // gfx950 CPol: nt, as the pointer form's nontemporal accesses
   __amdgpu_buffer_rsrc_t rsrc;
   __device__ __forceinline__ explicit ScrBuf(uint4 *base) {
     rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)Scr<K>::PER_WG, 0x00020000);
@@ -56,15 +60,11 @@ struct ScrBuf {
   }
   __device__ __forceinline__ void store(uint4 v, int lane, int half, int so) const {
     typedef int i32x4 __attribute__((ext_vector_type(4)));
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rsrc, lane * 32 + half * 16, so, AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rsrc, lane * 32 + half * 16 + so, 0, AUX);
   }
 };
-// which residual-scratch accesses go through the buffer resource (A/B probes of the round-3 finding that
-// the rsrc form gives different outputs): 262144 = loads only, 524288 = stores only, 1048576 = both (sc0 sc1)
 template <class K>
-constexpr bool kScrRsrcLd = (K::ABL & (65536 | 131072 | 262144 | 1048576)) != 0;
-template <class K>
-constexpr bool kScrRsrcSt = (K::ABL & (65536 | 131072 | 524288 | 1048576)) != 0;
+constexpr bool kScrRsrc = (K::ABL & 2097152) == 0;
 
 // In-place epilogue of a conv (or the stem): every wave has finished reading the buffer (barrier
 // before), out = relu(acc + bias (+ residual from scratch)) into the lane's own rows; SAVE also stores
@@ -84,7 +84,7 @@ __device__ __forceinline__ void epilogue(char *X, const f32x16 (&acc)[K::MT][K::
     if constexpr (RESID) {
 #pragma unroll
       for (int i = 0; i < HT; ++i) {
-        if constexpr (kScrRsrcLd<K>) {
+        if constexpr (kScrRsrc<K>) {
           const ScrBuf<K> sb(scr);
           const int so = ScrBuf<K>::soff(__builtin_amdgcn_readfirstlane(wave), m, t0 + i);
           res[i][0] = sb.load(lane, 0, so);
@@ -120,7 +120,7 @@ __device__ __forceinline__ void epilogue(char *X, const f32x16 (&acc)[K::MT][K::
       const uint4 lo = make_uint4(o[0], o[1], o[2], o[3]), hi = make_uint4(o[4], o[5], o[6], o[7]);
       *(uint4 *)p = lo;
       *(uint4 *)(p + 16) = hi;
-      if constexpr (SAVE && kScrRsrcSt<K>) {
+      if constexpr (SAVE && kScrRsrc<K>) {
         const ScrBuf<K> sb(scr);
         const int so = ScrBuf<K>::soff(__builtin_amdgcn_readfirstlane(wave), m, t);
         sb.store(lo, lane, 0, so);

@@ -26,6 +26,7 @@ evaluated by that network), or "random" / "lookahead" for the hard-coded
 players of games/general/hardcoded_players.py, optionally with its own
 `opponent_iterations`; `record=False` skips Move records (update=False).
 """
+import contextlib
 import os
 import time
 
@@ -438,11 +439,22 @@ class LanedEngine:
     game ids are offset by i * 2**40 (even, so swap_sides = id odd is preserved and ids stay unique).
     Each lane is a complete arena: results are those of `lanes` independent engines.  With `pack`
     the fused tower packs every lane's batch into full tiles (SPMCTS_TOWER_PACK) rather than whole
-    chip rounds, since the lanes' concurrent launches fill each other's partial rounds."""
+    chip rounds, since the lanes' concurrent launches fill each other's partial rounds.
+
+    `stagger` (default on, device-count evaluators): lane i runs i * S / lanes simulation steps behind
+    lane 0 (S = simulation steps per ply), so the lanes' ply boundaries -- the host round trips of
+    the move export and the first fill of the next searches (k_select_vl), whose slowest trees run
+    long serial chains of terminal simulations -- fall under another lane's tower launches instead of
+    coinciding.  Every lane still runs begin -> S steps -> move -> finish per ply on its own stream
+    (the same work in the same order: per-lane results are unchanged); only the interleaving of the
+    lanes changes.  A ply() call finishes one ply of every lane (lane i > 0: the one it began in the
+    previous call; on the first call it only begins one); `drain()` completes the plies staggered lanes have in flight (run() and
+    play_games() end with it, so they return at ply boundaries as before)."""
 
     GAME_ID_STRIDE = 1 << 40
 
-    def __init__(self, game, network, n_games=4096, lanes=2, seed=0, subsequence0=None, device=None, pack=True, **kw):
+    def __init__(self, game, network, n_games=4096, lanes=2, seed=0, subsequence0=None, device=None, pack=True,
+                 stagger=True, **kw):
         if lanes < 1 or n_games < lanes:
             raise ValueError(f"need 1 <= lanes <= n_games (lanes={lanes}, n_games={n_games})")
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -473,6 +485,8 @@ class LanedEngine:
                     if ev is not None and hasattr(ev, "concurrent"):
                         ev.concurrent = True
         self.n_games = n_games
+        self.stagger = bool(stagger) and lanes > 1
+        self._pending = False  # staggered lanes i > 0 are part-way through a ply
         self.iterations = self.lanes[0].iterations
         self.select_steps = self.lanes[0].select_steps
         self.search_threads = self.lanes[0].search_threads
@@ -524,13 +538,78 @@ class LanedEngine:
         self._lanes_wait_caller()
         self._each(lambda e: e.refresh_network())
 
+    def _stream(self, st):
+        return torch.cuda.stream(st) if st is not None else contextlib.nullcontext()
+
+    def _lags(self):
+        """Simulation steps lane i runs behind lane 0 when staggered."""
+        S, L = self.select_steps, len(self.lanes)
+        return [i * S // L for i in range(L)]
+
+    def _staggered(self):
+        return (getattr(self, "stagger", False) and 1 < len(self.lanes) <= self.select_steps
+                and all(e._device_count_ok() for e in self.lanes))
+
+    def _ply_staggered(self, on_moves, refill):
+        """One ply of every lane, lane i lag[i] steps behind lane 0: at global step lag[i] lane i > 0
+        ends the ply it began in the previous call (move, finish: the host reads its counts while lane
+        0's queued steps keep the chip busy) and begins the next; lane 0 runs a whole ply.  On the first
+        call (nothing in flight) lane i > 0 only begins its ply at step lag[i]."""
+        S, lag = self.select_steps, self._lags()
+        lanes, streams = self.lanes, self.streams
+        pending = getattr(self, "_pending", False)
+        res = [(0, 0)] * len(lanes)
+        with self._stream(streams[0]):
+            lanes[0]._ply_begin()
+        for t in range(S):
+            for i, (e, st) in enumerate(zip(lanes, streams)):
+                if i > 0 and t < lag[i] and not pending:
+                    continue  # first call: lane i has not begun yet
+                with self._stream(st):
+                    if i > 0 and t == lag[i]:
+                        if pending:  # the ply begun in the previous call ends here
+                            e._ply_move()
+                            res[i] = e._ply_finish(on_moves, refill, game_offset=i * self.GAME_ID_STRIDE)
+                        e._ply_begin()
+                    e._ply_simulation((t - lag[i]) % S)
+        with self._stream(streams[0]):
+            lanes[0]._ply_move()
+            res[0] = lanes[0]._ply_finish(on_moves, refill, game_offset=0)
+        self._pending = True
+        return res
+
+    def drain(self, on_moves=None, refill=True):
+        """Complete the plies that staggered lanes have in flight, so every lane stands at a ply boundary.
+        Returns (#games finished, #records exported) of those plies."""
+        if not getattr(self, "_pending", False):
+            return 0, 0
+        S, lag = self.select_steps, self._lags()
+        res = []
+        for i in range(1, len(self.lanes)):
+            e, st = self.lanes[i], self.streams[i]
+            with self._stream(st):
+                for s in range(S - lag[i], S):
+                    e._ply_simulation(s)
+                e._ply_move()
+                res.append(e._ply_finish(on_moves, refill, game_offset=i * self.GAME_ID_STRIDE))
+        self._pending = False
+        self._caller_waits_lanes()
+        return sum(r[0] for r in res), sum(r[1] for r in res)
+
+    def _caller_waits_lanes(self):
+        for st in self.streams:  # later work on the caller's stream sees every lane's work
+            if st is not None:
+                torch.cuda.current_stream(self.device).wait_stream(st)
+
     def ply(self, on_moves=None, refill=True):
         """One move of every active game of every lane. Returns (#games finished, #records exported)."""
         self._lanes_wait_caller()
-        if not all(e._device_count_ok() for e in self.lanes):  # host-synchronised evaluators: lane by lane
+        if self._staggered():
+            res = self._ply_staggered(on_moves, refill)
+        elif not all(e._device_count_ok() for e in self.lanes):  # host-synchronised evaluators: lane by lane
             res = []
             for i, (e, st) in enumerate(zip(self.lanes, self.streams)):
-                with torch.cuda.stream(st):
+                with self._stream(st):
                     res.append(e.ply(on_moves, refill, game_offset=i * self.GAME_ID_STRIDE))
         else:
             self._each(lambda e: e._ply_begin())
@@ -539,11 +618,9 @@ class LanedEngine:
             self._each(lambda e: e._ply_move())
             res = []
             for i, (e, st) in enumerate(zip(self.lanes, self.streams)):
-                with torch.cuda.stream(st):  # on_moves runs on the lane's stream, after its export
+                with self._stream(st):  # on_moves runs on the lane's stream, after its export
                     res.append(e._ply_finish(on_moves, refill, game_offset=i * self.GAME_ID_STRIDE))
-        for st in self.streams:  # later work on the caller's stream sees every lane's ply
-            if st is not None:
-                torch.cuda.current_stream(self.device).wait_stream(st)
+        self._caller_waits_lanes()
         return sum(r[0] for r in res), sum(r[1] for r in res)
 
     def run(self, plies=None, games=None, seconds=None, on_moves=None):
@@ -560,11 +637,19 @@ class LanedEngine:
                 break
             if self.max_games is not None and self.games_done >= self.max_games:
                 break
+        self.drain(on_moves=on_moves)  # staggered lanes finish the ply they have in flight
         return dict(plies=n, seconds=time.time() - t0, games=self.games_done, positions=self.positions)
 
     def play_games(self, n, on_moves=None, on_ply=None, exchange=None, every=8):
-        """As SelfPlayEngine.play_games, the n games split over the lanes (one exchange for all lanes)."""
+        """As SelfPlayEngine.play_games, the n games split over the lanes (one exchange for all lanes).
+        Staggered lanes start and end at ply boundaries: a ply a lane has in flight is completed first
+        (its records go into this call's exchange), and the ply each lane i > 0 has in flight when the
+        last round finds every rank done is completed before returning, its records sent in one more
+        (forced) exchange round, which every rank runs."""
         self._lanes_wait_caller()
+        ex = exchange if exchange is not None else distributed.MoveExchange(*self.lanes[0]._record_shape(),
+                                                                            sink=on_moves, every=every)
+        self.drain(on_moves=ex.stage)
         k = len(self.lanes)
         parts = [n // k + (1 if i < n % k else 0) for i in range(k)]
         targets = []
@@ -573,8 +658,6 @@ class LanedEngine:
                 targets.append(e._play_games_setup(m))
         if n <= 0 and not distributed.is_distributed():
             return 0
-        ex = exchange if exchange is not None else distributed.MoveExchange(*self.lanes[0]._record_shape(),
-                                                                            sink=on_moves, every=every)
         plies = 0
         while True:
             self.ply(on_moves=ex.stage)
@@ -585,6 +668,10 @@ class LanedEngine:
                            done=all(e.games_done >= t for e, t in zip(self.lanes, targets)))
             if r is not None and r[0]:
                 break
+        if getattr(self, "_pending", False):
+            self.drain(on_moves=ex.stage)
+            if distributed.is_distributed():  # every rank ended on the same round: one more, together
+                ex.end_ply(self.stats_vector, done=True, force=True)
         for e in self.lanes:
             e._started = e._limit
         return plies

@@ -230,6 +230,88 @@ def test_laned_engine_play_games_gloo():
                                 [1000 + i for i in range(4)] + [S + 1000 + i for i in range(4)])
 
 
+class _SeqLane(_FakeLane):
+    """A _FakeLane that records its phase calls (and checks a ply's steps run in order)."""
+
+    select_steps = 4
+    iterations = 4
+
+    def __init__(self, log, idx, **kw):
+        super().__init__(**kw)
+        self.log, self.idx = log, idx
+
+    def _ply_begin(self):
+        self.log.append((self.idx, "begin"))
+        self.sims = 0
+
+    def _ply_simulation(self, step=0):
+        assert step == self.sims, (self.idx, step, self.sims)
+        self.log.append((self.idx, step))
+        self.sims += 1
+
+    def _ply_move(self):
+        assert self.sims == self.select_steps
+        self.log.append((self.idx, "move"))
+
+    def _ply_finish(self, on_moves=None, refill=True, game_offset=0):
+        self.log.append((self.idx, "finish"))
+        return super()._ply_finish(on_moves if on_moves is not None else (lambda m: None), refill, game_offset)
+
+
+def _staggered_engine(log, rates=(1, 1)):
+    from self_play_reinforcement_learning_amd.engine import LanedEngine
+
+    eng = LanedEngine.__new__(LanedEngine)  # lanes without a GPU: no streams, fake arenas
+    eng.lanes = [_SeqLane(log, i, rate=r) for i, r in enumerate(rates)]
+    eng.streams = [None] * len(rates)
+    eng.select_steps = 4
+    eng.device = torch.device("cpu")
+    eng.stagger = True
+    eng._pending = False
+    return eng
+
+
+def test_staggered_lanes_keep_each_lanes_ply_order():
+    """LanedEngine(stagger=True): lane 1 runs S / 2 simulation steps behind lane 0, so its ply ends (move,
+    finish: the host round trip) and its next ply begins in the middle of lane 0's ply; each lane still runs
+    begin -> steps 0..S-1 -> move -> finish per ply, every call after the first finishes one ply of each
+    lane, and drain() completes lane 1's ply in flight."""
+    log = []
+    eng = _staggered_engine(log)
+    for _ in range(3):
+        eng.ply()
+    assert eng._pending
+    per = {i: [x for j, x in log if j == i] for i in (0, 1)}
+    ply = ["begin", 0, 1, 2, 3, "move", "finish"]
+    assert per[0] == ply * 3
+    assert per[1] == ply * 2 + ["begin", 0, 1]  # lane 1's third ply is in flight
+    # the interleaving: lane 1 finishes its ply after lane 0's step 2 of the next call (S = 4, lag 2)
+    call2 = log[log.index((0, "finish")) + 1:]
+    assert call2[:6] == [(0, "begin"), (0, 0), (1, 2), (0, 1), (1, 3), (0, 2)]
+    assert call2[6:9] == [(1, "move"), (1, "finish"), (1, "begin")]
+    eng.drain()
+    assert not eng._pending
+    per1 = [x for j, x in log if j == 1]
+    assert per1 == ply * 3 and [ln.plies_run for ln in eng.lanes] == [3, 3]
+
+
+def test_staggered_play_games_single_process():
+    """play_games with staggered lanes: a ply in flight is completed before the games are set up and after
+    the last ply, every game's records reach the sink once, and both lanes end at a ply boundary."""
+    log = []
+    eng = _staggered_engine(log, rates=(2, 1))
+    eng.ply()  # a ply() run leaves lane 1 part-way through its ply ...
+    assert eng._pending
+    got = []
+    eng.play_games(6, on_moves=lambda m: got.extend(m["game"].tolist()))  # ... play_games completes it first
+    assert not eng._pending
+    assert [ln.games_done for ln in eng.lanes] == [3, 3]
+    S = eng.GAME_ID_STRIDE
+    assert sorted(got) == sorted([0, 1, 2] + [S + i for i in range(3)])
+    per1 = [x for j, x in log if j == 1]
+    assert per1 == ["begin", 0, 1, 2, 3, "move", "finish"] * eng.lanes[1].plies_run
+
+
 def test_pack_unpack_roundtrip():
     m = _moves(0, 9)
     back = D.unpack_moves(D.pack_moves(m), 42, 7)

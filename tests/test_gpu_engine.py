@@ -187,10 +187,23 @@ def test_trainer_graph_matches_eager_steps(autocast):
     """The captured-graph update (_Trainer(graph=True): forward, AZ loss, backward and the SGD step as
     one HIP graph replayed per step) gives the weights of the same updates run eagerly, step for step:
     3 eager warm-up steps, the capture, replays; a learning-rate change (ReduceLROnPlateau) re-captures
-    and the new rate takes effect.  Eval-mode dropout (the masks' RNG is drawn differently inside a graph)."""
+    and the new rate takes effect.  Eval-mode dropout (the masks' RNG is drawn differently inside a graph).
+    With MIOpen's default algorithm choice two EAGER runs differ (atomics in the fp16 backward kernels:
+    up to 5 % of an update, profiles/r04/trainer/determinism_default.json); with deterministic
+    algorithms requested, eager, replayed and repeated runs are bit-identical
+    (determinism_deterministic.json), so the test asks for them and compares bit for bit."""
     from self_play_reinforcement_learning_amd.modules import ResidualTower
     from self_play_reinforcement_learning_amd.self_play_parallel import _Trainer
 
+    det = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        _graph_vs_eager(autocast, _Trainer, ResidualTower)
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det
+
+
+def _graph_vs_eager(autocast, _Trainer, ResidualTower):
     g = torch.Generator().manual_seed(7)
     rows = dict(state=torch.randint(-1, 2, (512, 42), dtype=torch.int8, generator=g),
                 tree_probs=torch.softmax(torch.randn(512, 7, generator=g), 1),
@@ -200,7 +213,6 @@ def test_trainer_graph_matches_eager_steps(autocast):
     for graph in (False, True):
         torch.manual_seed(0)
         net = ResidualTower(7, 6, 7, num_blocks=2, filter_factor=16).cuda()
-        w_init = {k: v.clone() for k, v in net.state_dict().items()}
         opt = torch.optim.SGD(net.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
         tr = _Trainer(net, opt, memory_size=1000, batch_size=64, min_memory=0, q_average=True, device="cuda",
                       overlap=False, autocast=autocast, train_mode=False, graph=graph)
@@ -219,22 +231,9 @@ def test_trainer_graph_matches_eager_steps(autocast):
         out.append(({k: v.clone() for k, v in net.state_dict().items()}, losses))
     (w0, l0), (w1, l1) = out
     assert all(math.isfinite(x) for x in l1)
-    assert max(abs(a - b) for a, b in zip(l0, l1)) < 1e-4 * max(abs(x) for x in l0), (l0, l1)
-    # the replayed kernels need not be the eager ones bit for bit (MIOpen may pick another algorithm under
-    # capture, and its fp16 kernels round differently): each tensor's total update over the 10 steps must
-    # agree to 1e-3 of its norm in fp32 and to 5e-2 under fp16 autocast (one step lost or repeated would
-    # move it by ~1e-1)
-    tol = 5e-2 if autocast else 1e-3
-    rel = {}
+    assert l0 == l1, (l0, l1)
     for k in w0:
-        if not w0[k].is_floating_point():
-            assert torch.equal(w0[k], w1[k]), k
-            continue
-        d0, d1 = (w0[k] - w_init[k]).double(), (w1[k] - w_init[k]).double()
-        rel[k] = (d0 - d1).norm().item() / (d0.norm().item() + 1e-12)
-    print("graph vs eager, update rel. difference: max", max(rel.values()), "median", sorted(rel.values())[len(rel) // 2])
-    bad = {k: r for k, r in rel.items() if r > tol}
-    assert not bad, bad
+        assert torch.equal(w0[k], w1[k]), k
 
 
 def test_trainer_graph_train_mode_replays_run():
