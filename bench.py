@@ -236,9 +236,9 @@ def main():
                     help="arenas per GPU on their own HIP streams (engine.LanedEngine); 1 = one arena")
     ap.add_argument("--blocks-per-tree", type=int, default=0,
                     help="node blocks per tree; below the worst case the arena recycles subtrees (k_compact)")
-    ap.add_argument("--no-stagger", action="store_true",
-                    help="lanes in lock step (every lane's ply boundary at the same time) instead of lane i "
-                         "i * S / lanes simulation steps behind lane 0 (engine.LanedEngine stagger)")
+    ap.add_argument("--stagger", action="store_true",
+                    help="lane i runs i * S / lanes simulation steps behind lane 0 (engine.LanedEngine stagger) "
+                         "instead of the lanes in lock step")
     ap.add_argument("--no-pack", action="store_true",
                     help="lanes > 1: keep round-aligned tower tiles (no SPMCTS_TOWER_PACK)")
     ap.add_argument("--twin-no-dedup", type=int, default=5, metavar="PLIES",
@@ -304,7 +304,7 @@ def main():
               blocks_per_tree=args.blocks_per_tree, leaf_dedup=False if args.no_leaf_dedup else None)
     if args.lanes > 1:
         eng = LanedEngine("connect4", net, n_games=args.games, lanes=args.lanes, pack=not args.no_pack,
-                          stagger=not args.no_stagger, **kw)
+                          stagger=args.stagger, **kw)
     else:
         eng = SelfPlayEngine("connect4", net, n_games=args.games, **kw)
     gathered = []
@@ -566,7 +566,7 @@ def main():
         kw2 = dict(kw, dtype={"bf16": torch.bfloat16, "fp16": torch.float16}[other])
         if args.lanes > 1:
             eng2 = LanedEngine("connect4", net, n_games=args.games, lanes=args.lanes, pack=not args.no_pack,
-                               stagger=not args.no_stagger, **kw2)
+                               stagger=args.stagger, **kw2)
         else:
             eng2 = SelfPlayEngine("connect4", net, n_games=args.games, **kw2)
         ex2 = D.MoveExchange(42, 7, sink=lambda g: None, every=args.exchange_every)

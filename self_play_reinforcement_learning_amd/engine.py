@@ -441,20 +441,22 @@ class LanedEngine:
     the fused tower packs every lane's batch into full tiles (SPMCTS_TOWER_PACK) rather than whole
     chip rounds, since the lanes' concurrent launches fill each other's partial rounds.
 
-    `stagger` (default on, device-count evaluators): lane i runs i * S / lanes simulation steps behind
+    `stagger` (off by default; device-count evaluators): lane i runs i * S / lanes simulation steps behind
     lane 0 (S = simulation steps per ply), so the lanes' ply boundaries -- the host round trips of
     the move export and the first fill of the next searches (k_select_vl), whose slowest trees run
     long serial chains of terminal simulations -- fall under another lane's tower launches instead of
     coinciding.  Every lane still runs begin -> S steps -> move -> finish per ply on its own stream
     (the same work in the same order: per-lane results are unchanged); only the interleaving of the
     lanes changes.  A ply() call finishes one ply of every lane (lane i > 0: the one it began in the
-    previous call; on the first call it only begins one); `drain()` completes the plies staggered lanes have in flight (run() and
-    play_games() end with it, so they return at ply boundaries as before)."""
+    previous call; on the first call it only begins one); `drain()` completes the plies staggered lanes
+    have in flight (run() and play_games() end with it, so they return at ply boundaries as before).
+    Measured on one box (profiles/r04/stagger/): ply-start tower-free time 1.6 % -> 0.8 % of a
+    steady-state ply, steady-state positions/s +0.4 %, the driver's short run -0.6 %: off by default."""
 
     GAME_ID_STRIDE = 1 << 40
 
     def __init__(self, game, network, n_games=4096, lanes=2, seed=0, subsequence0=None, device=None, pack=True,
-                 stagger=True, **kw):
+                 stagger=False, **kw):
         if lanes < 1 or n_games < lanes:
             raise ValueError(f"need 1 <= lanes <= n_games (lanes={lanes}, n_games={n_games})")
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())

@@ -510,10 +510,12 @@ def test_device_errors_are_raised():
     a.close()
 
 
-def test_laned_engine_plays_like_its_lanes():
+@pytest.mark.parametrize("stagger", [False, True])
+def test_laned_engine_plays_like_its_lanes(stagger):
     """LanedEngine = independent lane arenas on their own streams: per-lane results equal those of a
     SelfPlayEngine with the same slots, seed and Philox subsequences, counters add up, and exported
-    game ids are unique with the swap_sides parity preserved."""
+    game ids are unique with the swap_sides parity preserved -- with the lanes in lock step and
+    staggered (lane 1 half a ply behind lane 0; run() ends with drain())."""
     import numpy as np
 
     from self_play_reinforcement_learning_amd.engine import LanedEngine, SelfPlayEngine
@@ -521,7 +523,7 @@ def test_laned_engine_plays_like_its_lanes():
 
     torch.manual_seed(0)
     net = ResidualTower(7, 6, 7, num_blocks=1, filter_factor=32).cuda().eval()
-    laned = LanedEngine("connect4", net, n_games=40, lanes=2, iterations=12, seed=3)
+    laned = LanedEngine("connect4", net, n_games=40, lanes=2, iterations=12, seed=3, stagger=stagger)
     got = []
     laned.run(plies=30, on_moves=lambda m: got.append({k: v.cpu().numpy() for k, v in m.items()}))
     laned.check()
