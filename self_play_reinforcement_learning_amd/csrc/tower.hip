@@ -688,7 +688,16 @@ __device__ __forceinline__ void conv_tap_x(const char *src, const Nbr<K> &nb, f3
       for (int m = 0; m < K::MT; ++m)
         a[slot][m] = wb.template load<WAUX>(wn_off + m * MSTRIDE + (uint32_t)(sn - STEPS) * 1024u);
     }
-    if (TAP == 0 && kk == 0) {
+    if constexpr (K::ABL & 4194304) {
+      // A/B: weight-major MFMA order (the same A operand for NTA consecutive MFMAs; each accumulator's
+      // k order is unchanged, so the outputs are bit-identical) -- an operand-toggling / clock probe
+#pragma unroll
+      for (int m = 0; m < K::MT; ++m)
+#pragma unroll
+        for (int t = 0; t < K::NT; ++t)
+          if ((LV >> t) & 1u)
+            acc[m][t] = (TAP == 0 && kk == 0) ? K::mfma(acur[m], bc[t], f32x16{}) : K::mfma(acur[m], bc[t], acc[m][t]);
+    } else if (TAP == 0 && kk == 0) {
 #pragma unroll
       for (int t = 0; t < K::NT; ++t)
 #pragma unroll
@@ -1032,7 +1041,7 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
     const int wn_steps = L + 1 < n_convs ? LSTEPS : 0;
     if constexpr (K::XMAJ) {
       static_assert(K::ONEBUF || ((K::MG == 2 || (K::MG == 1 && K::EDGE)) &&
-                        (K::ABL & ~(2 | 4 | 8 | 16 | 128 | 512 | 4096 | 8192 | 16384)) == 0 && (K::ABL == 0 || K::EDGE)),
+                        (K::ABL & ~(2 | 4 | 8 | 16 | 128 | 512 | 4096 | 8192 | 16384 | 4194304)) == 0 && (K::ABL == 0 || K::EDGE)),
                     "column-group conv: two row halves (edge tiles: or one); edge tiles take the 2/4/8/16/128 timing ablations");
       const bool even = (L & 1) == 0;
       if constexpr (K::MG == 1) {
@@ -1683,6 +1692,8 @@ static int forward_ab(int32_t width, int32_t height, int32_t channels, int32_t n
       ABLATE_EDGE(0) ABLATE_EDGE(2) ABLATE_EDGE(4) ABLATE_EDGE(6) ABLATE_EDGE(8) ABLATE_EDGE(16) ABLATE_EDGE(24)
       ABLATE_EDGE(30) ABLATE_EDGE(128) ABLATE_EDGE(512)
       case 301: return launch<Cfg<128, 256, 7, 6, 2, 4, 4096, 4, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      // weight-major MFMA order within a k-step (bit-identical; clock / operand-toggling probe)
+      case 304: return launch<Cfg<128, 256, 7, 6, 2, 4, 4194304, 4, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       case 302: return launch<Cfg<128, 256, 7, 6, 2, 4, 8192, 4, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       case 316: return launch<Cfg<128, 256, 7, 6, 2, 4, 16384, 4, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
 #undef ABLATE_EDGE
