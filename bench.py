@@ -249,9 +249,12 @@ def main():
     ap.add_argument("--dtype", choices=["bf16", "fp16"], default="fp16",
                     help="element type of the fused trunk's weights / activations (fp32 accumulation); fp16 (the "
                          "default) is the reference's own inference dtype (amp.autocast, inference_worker.py:117)")
-    ap.add_argument("--no-secondary", dest="secondary", action="store_false",
-                    help="skip the secondary line: the other trunk dtype (bf16 <-> fp16) on a fresh engine with the "
-                         "same seeds, --warmup and --steps, reported as secondary_dtype")
+    ap.add_argument("--secondary", action="store_true",
+                    help="also time the other trunk dtype (bf16 <-> fp16) on a fresh engine with the same seeds, "
+                         "--warmup and --steps, reported as secondary_dtype.  Off by default: bf16's search shift is "
+                         "pinned only at 0.03 (tests/test_gpu_statistical.py SHIFT_TOL), a bound that does not reject "
+                         "a serial search, so the headline runs fp16 alone")
+    ap.add_argument("--no-secondary", dest="secondary", action="store_false", help=argparse.SUPPRESS)
     ap.add_argument("--search-threads", type=int, default=4,
                     help="sims in flight per tree with virtual loss: the reference's thread_count search "
                          "(mcts.py:328-331), 4 in its headline self-play setup (InferenceProxy workers, "

@@ -63,15 +63,20 @@ def run(args, updates, overlap, autocast=True, graph=True):
                 replay_rows=len(tr.memory), last_loss=loss)
 
 
-def trainer_only(args, graph, autocast=True, steps=40):
-    """ms per SGD step of the trainer alone (batch 64, ResNet-128x20, train mode), graphed or eager."""
+def trainer_only(args, graph, autocast=True, steps=40, channels_last=False, benchmark=False):
+    """ms per SGD step of the trainer alone (batch 64, ResNet-128x20, train mode), graphed or eager;
+    `channels_last`: the network's tensors in NHWC order; `benchmark`: MIOpen's exhaustive kernel search
+    (torch.backends.cudnn.benchmark)."""
     import torch
 
     from self_play_reinforcement_learning_amd.modules import ResidualTower
     from self_play_reinforcement_learning_amd.self_play_parallel import _Trainer
 
+    torch.backends.cudnn.benchmark = bool(benchmark)
     torch.manual_seed(0)
     net = ResidualTower(7, 6, 7, num_blocks=20, filter_factor=32).cuda()
+    if channels_last:
+        net = net.to(memory_format=torch.channels_last)
     tr = _Trainer(net, torch.optim.SGD(net.parameters(), lr=0.001, momentum=0.9, weight_decay=1e-4), memory_size=200000,
                   batch_size=64, min_memory=0, q_average=True, device="cuda", overlap=True, autocast=autocast,
                   graph=graph)
@@ -90,8 +95,9 @@ def trainer_only(args, graph, autocast=True, steps=40):
     tr.sync()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    return dict(train_graph=graph, train_autocast=autocast, steps=steps, ms_per_sgd_step=dt / steps * 1e3,
-                graph_captures=tr.graph_captures, last_loss=float(tr.last_loss))
+    torch.backends.cudnn.benchmark = False
+    return dict(train_graph=graph, train_autocast=autocast, channels_last=channels_last, benchmark=benchmark, steps=steps,
+                ms_per_sgd_step=dt / steps * 1e3, graph_captures=tr.graph_captures, last_loss=float(tr.last_loss))
 
 
 def main():
@@ -101,7 +107,15 @@ def main():
     ap.add_argument("--games", type=int, default=4096)
     ap.add_argument("--sims", type=int, default=200)
     ap.add_argument("--min-memory", type=int, default=20000)
+    ap.add_argument("--trainer-variants", action="store_true",
+                    help="trainer-only timings of graphed steps with NHWC tensors and MIOpen's exhaustive search, "
+                         "no self-play runs")
     args = ap.parse_args()
+    if args.trainer_variants:
+        rows = [trainer_only(args, True, autocast=a, channels_last=c, benchmark=b)
+                for a in (True, False) for c in (False, True) for b in (False, True)]
+        print(json.dumps(dict(trainer_only=rows)), flush=True)
+        return
     out = dict(workload=f"connect4 self-play + training, {args.sims} sims, {args.games} games, ResNet-128x20 (bf16 "
                         f"trunk for leaves, SGD batch 64 under fp16 autocast as updateworker.py:148, or fp32), K = 4, two lanes",
                trainer_only=[trainer_only(args, True), trainer_only(args, False), trainer_only(args, True, False)],

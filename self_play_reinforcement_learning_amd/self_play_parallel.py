@@ -93,7 +93,7 @@ class SelfPlayScheduler:
                  save_dir="saves", epoch_length=500, initial_games=64, lr=0.001, stagger=False, evaluation_games=100,
                  evaluation_network=None, stagger_mem_step=5000, deduplicate=False, update_delay=0.01,
                  self_play=None, n_games=None, device=None, seed=0, updates_per_ply=4, lanes=None, exchange_every=8,
-                 gpus=None, start_time=None, overlap_training=True, train_autocast=True, train_graph=True):
+                 gpus=None, start_time=None, overlap_training=False, train_autocast=True, train_graph=True):
         # constructor arguments, for rank processes started by this scheduler (_run_ranks)
         self._init_kwargs = {k: v for k, v in locals().items() if k not in ("self", "__class__")}
         self.policy_container = policy_container
@@ -115,7 +115,10 @@ class SelfPlayScheduler:
         self.network = self._get_network(network, policy_container)
         self.seed = seed
         self.updates_per_ply = updates_per_ply
-        # the trainer's SGD steps on a HIP stream of their own, beside the arena's plies (_Trainer)
+        # True: the trainer's SGD steps on a HIP stream of their own, beside the arena's plies (_Trainer).
+        # Off by default: with the graphed step the arena keeps the GPU busy either way and the steps
+        # ordered on the plies' stream measured faster (18.1k vs 17.7k positions/s at 4 steps per ply,
+        # profiles/r04/trainer/train_throughput.json)
         self.overlap_training = overlap_training
         # the UpdateWorker's update_from_memory runs under torch.cuda.amp.autocast() (fp16 on CUDA, no
         # GradScaler; updateworker.py:148); False trains in fp32

@@ -280,7 +280,13 @@ def test_sequential_search_matches_reference_resnet(pi):
 # streams, and within 4.5 SE + TOL of the reference's own threaded samples (G6 resnet_single, 1,000
 # searches per position).  fp16 (the reference's inference dtype) keeps 11 significand bits; bf16 keeps
 # 8 and moves this net's small values (std 0.037) by ~0.002 (scripts/tower_err.py), 8x fp16's error.
-SHIFT_TOL = {"fp16": 0.01, "bf16": 0.03}
+# Measured (scripts/diag/shift_excess.py, profiles/r04/shift_excess.json; the searches are deterministic:
+# fixed Philox seeds, batch-independent trunk): fp16 moves the mean visit fractions by <= 0.0007 from the
+# fp32-evaluator search, bf16 by up to 0.0157 (G6 position 2); the negative controls lie at max excess
+# over 4.5 SE of 0.0114 / 0.0235 (serial search, fp16 / bf16) and 0.10 (half budget).  Round 3's bf16 bound
+# of 0.03 did not reject the serial search; 0.02 passes bf16 and rejects it.  bf16 is not the headline
+# dtype (bench.py --dtype fp16; --secondary adds a bf16 line on request).
+SHIFT_TOL = {"fp16": 0.01, "bf16": 0.02}
 
 
 @pytest.mark.parametrize("precision", ["fp16", "bf16"])
@@ -306,7 +312,7 @@ def test_fused_tower_search_shift(pi, precision):
 @pytest.mark.parametrize("variant", ["sims100", "serial"])
 def test_resnet_statistical_check_has_power(variant, precision):
     """Negative control at the headline net: the fused-tower comparison at its stated bound (4.5 SE +
-    SHIFT_TOL: 0.01 for fp16, the bench's default dtype; 0.03 for bf16, the bench's secondary line)
+    SHIFT_TOL: 0.01 for fp16, the bench's dtype; 0.02 for bf16, bench.py --dtype bf16 / --secondary)
     rejects, against the reference's threaded ResNet samples, a search with half the simulation budget
     (100 instead of 200) and one run serially (1 simulation in flight instead of the reference's
     thread_count with virtual loss, mcts.py:229-262).  Root noise drawn with Dirichlet alpha 0.3 instead
