@@ -110,7 +110,12 @@ def main():
     ap.add_argument("--trainer-variants", action="store_true",
                     help="trainer-only timings of graphed steps with NHWC tensors and MIOpen's exhaustive search, "
                          "no self-play runs")
+    ap.add_argument("--trainer-only-graph", action="store_true",
+                    help="only the graphed fp16-autocast trainer-only timing (for a kernel trace)")
     args = ap.parse_args()
+    if args.trainer_only_graph:
+        print(json.dumps(dict(trainer_only=[trainer_only(args, True, steps=100)])), flush=True)
+        return
     if args.trainer_variants:
         rows = [trainer_only(args, True, autocast=a, channels_last=c, benchmark=b)
                 for a in (True, False) for c in (False, True) for b in (False, True)]

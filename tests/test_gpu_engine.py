@@ -688,7 +688,8 @@ def test_leaf_dedup_two_networks_exact():
 def test_bench_line_small_with_no_dedup_twin():
     """bench.py end to end on a small workload (subprocess, as the driver runs it): one JSON line with
     the contract keys, roofline and tree roofline, and the --twin-no-dedup plies (leaf dedup off on
-    the same arenas: one network row per leaf)."""
+    the same arenas: one network row per leaf), and with --secondary the bf16 trunk's line on a fresh
+    engine."""
     import json
     import os
     import subprocess
@@ -696,7 +697,7 @@ def test_bench_line_small_with_no_dedup_twin():
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, os.path.join(root, "bench.py"), "--games", "512", "--sims", "16", "--blocks", "2",
-           "--steps", "3", "--warmup", "2", "--no-cpu-baseline", "--twin-no-dedup", "2"]
+           "--steps", "3", "--warmup", "2", "--no-cpu-baseline", "--twin-no-dedup", "2", "--secondary"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=root, check=True).stdout
     line = [l for l in out.splitlines() if l.startswith("{")]
     assert len(line) == 1
@@ -708,7 +709,7 @@ def test_bench_line_small_with_no_dedup_twin():
     assert 0 < d["roofline"]["frac"] < 1 and d["config"]["leaf_dedup"] is True and d["nn"]["rows_per_leaf"] <= 1.0
     tw = d["no_dedup_twin"]
     assert tw["plies"] == 2 and tw["value"] > 0 and tw["rows_per_leaf"] == 1.0
-    # the default dtype is the reference's fp16; the bf16 trunk is timed on the same games afterwards
+    # the default dtype is the reference's fp16; --secondary times the bf16 trunk on a fresh engine afterwards
     assert d["dtype"] == "fp16" and d["secondary_dtype"]["dtype"] == "bf16" and d["secondary_dtype"]["value"] > 0
     r = d["ranks"]
     assert r["world_size"] == 1 and len(r["per_rank"]) == 1
