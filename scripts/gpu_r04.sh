@@ -17,8 +17,9 @@ if [[ " $ST " == *" bench "* ]]; then
   timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
   python -c "
 import json; d=json.loads([l for l in open('$O/bench.json') if l.startswith('{')][0])
+sec = d.get('secondary_dtype')
 print('bench', d['dtype'], round(d['value']), round(d['roofline']['frac'],4), 'twin', round(d['no_dedup_twin']['value']),
-      'secondary', d['secondary_dtype']['dtype'], round(d['secondary_dtype']['value']), round(d['secondary_dtype']['roofline']['frac'],4),
+      'secondary', (sec['dtype'], round(sec['value']), round(sec['roofline']['frac'],4)) if sec else None,
       'cpu', round(d['cpu_baseline']['value'],2))"
 fi
 if [[ " $ST " == *" train "* ]]; then
