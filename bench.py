@@ -43,8 +43,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 TRAFFIC_FILE = os.path.join(HERE, "profiles", "r01_bench_prof", "k_tower_traffic.json")  # --search-threads 1
-TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r03_bench_prof", "k_tower_traffic.json")  # 4 (default)
-TREE_TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r03_tree_pmc", "tree_traffic.json")
+TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r04_bench_prof", "k_tower_traffic.json")  # 4 (default)
+TREE_TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r04_tree_pmc", "tree_traffic.json")
+# in-bench clock and MFMA-busy share of the timed k_tower_dyn dispatches (one PMC pass per trunk dtype,
+# scripts/gpu_prof_r04.sh -> scripts/tower_util.py): the roofline's frac = busy x clock / 2.4 GHz / 0.833
+CLOCK_FILES = {d: os.path.join(HERE, "profiles", "r04_bench_prof", f"tower_util_bench_{d}.json") for d in ("fp16", "bf16")}
 
 # MI355X reference figures (/opt/skills/guides/MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
@@ -419,6 +422,21 @@ def main():
         traffic = tj.get("bytes_per_dispatch", tj["bytes_per_launch"]) * max(1, args.lanes)
         traffic_src = os.path.relpath(tfile, HERE)
 
+    # the committed in-bench PMC pass of this trunk dtype (bench.py cannot run the profiler itself)
+    clock = None
+    cfile = CLOCK_FILES.get(args.dtype)
+    if cfile and os.path.exists(cfile) and (args.games, args.sims, args.filter_factor, args.blocks) == (4096, 200, 32, 20):
+        with open(cfile) as f:
+            cj = json.load(f)
+        ghz, busy = cj["clock_ghz_weighted"], cj["mfma_busy_frac_weighted"]
+        clock = {"clock_ghz": ghz, "mfma_busy_frac": busy, "dispatches": cj.get("dispatches"),
+                 "source": os.path.relpath(cfile, HERE),
+                 "peak_at_clock": BF16_DENSE_PEAK_TFLOPS * ghz / 2.4,
+                 "frac_at_clock": tw_tflops / (BF16_DENSE_PEAK_TFLOPS * ghz / 2.4),
+                 "note": "peak scaled to the clock the chip held under this kernel (GRBM_GUI_ACTIVE / 8 / duration, "
+                         "profiled run of this command); frac ~ busy x clock/2.4 / 0.833 (edge tiles skip 16.7 % of "
+                         "the dense MFMAs)"}
+
     out = {
         "metric": f"self-play positions/sec (Connect4, {args.sims} sims/move)",
         "value": moves_all / elapsed_max,
@@ -464,6 +482,7 @@ def main():
                            "duration = their union busy time" if lanes > 1 else "one k_tower_dyn dispatch"),
             "avg_dispatch_us": tw_sum_ms / max(1, tw_dispatches) * 1e3,
             "dispatches": tw_dispatches,
+            "clock": clock,
         },
         "tree_roofline": {
             "kernel": ("k_select<C4> + k_expand<C4> (PUCT tree walk, backup)" if args.search_threads <= 1 else

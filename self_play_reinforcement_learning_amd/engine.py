@@ -553,10 +553,12 @@ class LanedEngine:
                 and all(e._device_count_ok() for e in self.lanes))
 
     def _ply_staggered(self, on_moves, refill):
-        """One ply of every lane, lane i lag[i] steps behind lane 0: at global step lag[i] lane i > 0
-        ends the ply it began in the previous call (move, finish: the host reads its counts while lane
-        0's queued steps keep the chip busy) and begins the next; lane 0 runs a whole ply.  On the first
-        call (nothing in flight) lane i > 0 only begins its ply at step lag[i]."""
+        """One ply of every lane, lane i lag[i] steps behind lane 0.  Issue order (each stream keeps its
+        own op order, so per-lane results are unchanged): lane 0's whole ply up to its move, interleaved
+        with the last lag[i] steps of the ply lane i > 0 began in the previous call; then lane i's move
+        and finish (the host reads its counts while lane 0's queued half ply keeps the chip busy) and
+        the first S - lag[i] steps of its next ply; then lane 0's finish (lane i's queued steps keep the
+        chip busy).  On the first call (nothing in flight) lane i > 0 only begins its ply."""
         S, lag = self.select_steps, self._lags()
         lanes, streams = self.lanes, self.streams
         pending = getattr(self, "_pending", False)
@@ -565,17 +567,23 @@ class LanedEngine:
             lanes[0]._ply_begin()
         for t in range(S):
             for i, (e, st) in enumerate(zip(lanes, streams)):
-                if i > 0 and t < lag[i] and not pending:
-                    continue  # first call: lane i has not begun yet
                 with self._stream(st):
-                    if i > 0 and t == lag[i]:
-                        if pending:  # the ply begun in the previous call ends here
-                            e._ply_move()
-                            res[i] = e._ply_finish(on_moves, refill, game_offset=i * self.GAME_ID_STRIDE)
-                        e._ply_begin()
-                    e._ply_simulation((t - lag[i]) % S)
+                    if i == 0:
+                        e._ply_simulation(t)
+                    elif pending and t < lag[i]:  # the ply begun in the previous call
+                        e._ply_simulation(S - lag[i] + t)
         with self._stream(streams[0]):
             lanes[0]._ply_move()
+        for i in range(1, len(lanes)):
+            e = lanes[i]
+            with self._stream(streams[i]):
+                if pending:
+                    e._ply_move()
+                    res[i] = e._ply_finish(on_moves, refill, game_offset=i * self.GAME_ID_STRIDE)
+                e._ply_begin()
+                for s in range(S - lag[i]):
+                    e._ply_simulation(s)
+        with self._stream(streams[0]):
             res[0] = lanes[0]._ply_finish(on_moves, refill, game_offset=0)
         self._pending = True
         return res

@@ -285,10 +285,12 @@ def test_staggered_lanes_keep_each_lanes_ply_order():
     ply = ["begin", 0, 1, 2, 3, "move", "finish"]
     assert per[0] == ply * 3
     assert per[1] == ply * 2 + ["begin", 0, 1]  # lane 1's third ply is in flight
-    # the interleaving: lane 1 finishes its ply after lane 0's step 2 of the next call (S = 4, lag 2)
+    # the issue order of a call (S = 4, lag 2): lane 0's ply up to its move with lane 1's last 2 steps,
+    # then lane 1's move, finish, next begin and its first 2 steps, then lane 0's finish
     call2 = log[log.index((0, "finish")) + 1:]
-    assert call2[:6] == [(0, "begin"), (0, 0), (1, 2), (0, 1), (1, 3), (0, 2)]
-    assert call2[6:9] == [(1, "move"), (1, "finish"), (1, "begin")]
+    assert call2[:11] == [(0, "begin"), (0, 0), (1, 2), (0, 1), (1, 3), (0, 2), (0, 3), (0, "move"),
+                          (1, "move"), (1, "finish"), (1, "begin")]
+    assert call2[11:14] == [(1, 0), (1, 1), (0, "finish")]
     eng.drain()
     assert not eng._pending
     per1 = [x for j, x in log if j == 1]
