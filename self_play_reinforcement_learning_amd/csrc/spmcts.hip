@@ -1071,8 +1071,11 @@ __global__ __launch_bounds__(256) void k_dedup_alias(View v) {
 }
 
 __global__ __launch_bounds__(1024) void k_scan_need(View v, int32_t *count_out) {
-  __shared__ int32_t s_p0[1024], s_p1[1024];
-  const int tid = threadIdx.x;
+  // wave totals of the two segments' owner counts (a two-level scan: 6 shuffle steps within each wave,
+  // 4 over the 16 wave totals, 2 barriers; the round-3 1,024-entry Hillis-Steele scan took 20 barriers
+  // and 8 KB of LDS, and ran 30-40 us beside a trunk workgroup whose waves hold the SIMDs' issue slots)
+  __shared__ int32_t s_w0[16], s_w1[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T = v.NS;  // pending slots (tree * K + j), tree order then in-flight order
   const int chunk = (T + 1023) / 1024;
   const int lo = min(T, tid * chunk), hi = min(T, lo + chunk);
@@ -1083,19 +1086,40 @@ __global__ __launch_bounds__(1024) void k_scan_need(View v, int32_t *count_out) 
     if (row_owner(v, t)) {
       if (v.tnet[t / v.K]) ++c1; else ++c0;
     }
-  s_p0[tid] = c0;
-  s_p1[tid] = c1;
-  __syncthreads();
-  // inclusive Hillis-Steele scans over 1024 partials
-  for (int off = 1; off < 1024; off <<= 1) {
-    const int a0 = tid >= off ? s_p0[tid - off] : 0;
-    const int a1 = tid >= off ? s_p1[tid - off] : 0;
-    __syncthreads();
-    s_p0[tid] += a0;
-    s_p1[tid] += a1;
-    __syncthreads();
+  // inclusive scans of (c0, c1) in thread order: within the wave, then over the wave totals
+  int i0 = c0, i1 = c1;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int a0 = __shfl_up(i0, off, 64), a1 = __shfl_up(i1, off, 64);
+    if (lane >= off) {
+      i0 += a0;
+      i1 += a1;
+    }
   }
-  int r0 = s_p0[tid] - c0, r1 = v.seg1 + s_p1[tid] - c1;
+  if (lane == 63) {
+    s_w0[wave] = i0;
+    s_w1[wave] = i1;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    int w0 = lane < 16 ? s_w0[lane] : 0, w1 = lane < 16 ? s_w1[lane] : 0;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) {
+      const int a0 = __shfl_up(w0, off, 64), a1 = __shfl_up(w1, off, 64);
+      if (lane >= off) {
+        w0 += a0;
+        w1 += a1;
+      }
+    }
+    if (lane < 16) {
+      s_w0[lane] = w0;
+      s_w1[lane] = w1;
+    }
+  }
+  __syncthreads();
+  i0 += wave ? s_w0[wave - 1] : 0;
+  i1 += wave ? s_w1[wave - 1] : 0;
+  int r0 = i0 - c0, r1 = v.seg1 + i1 - c1;
 #pragma unroll 16
   for (int t = lo; t < hi; ++t)
     if (row_owner(v, t)) {
@@ -1103,14 +1127,14 @@ __global__ __launch_bounds__(1024) void k_scan_need(View v, int32_t *count_out) 
       v.row_tree[r] = t;
       if (v.K > 1) v.srow[t] = r;
     }
-  if (tid == 1023) {
-    v.row_count[0] = s_p0[1023];
-    v.row_count[1] = s_p1[1023];
-    v.gcnt[10] += s_p0[1023] + s_p1[1023];  // network rows emitted (counters.nn_rows)
+  if (tid == 1023) {  // the last thread's inclusive prefix is each segment's total
+    v.row_count[0] = i0;
+    v.row_count[1] = i1;
+    v.gcnt[10] += i0 + i1;  // network rows emitted (counters.nn_rows)
     if (count_out) {
-      count_out[0] = s_p0[1023] + s_p1[1023];
-      count_out[1] = s_p0[1023];
-      count_out[2] = s_p1[1023];
+      count_out[0] = i0 + i1;
+      count_out[1] = i0;
+      count_out[2] = i1;
     }
   }
 }
