@@ -627,6 +627,22 @@ struct XLive {
 
 // One tap of a column-major / edge-tile layer with per-tap live tiles (Cfg::EDGE): conv_group_x's
 // pipeline for one tap; the B fragments of the next tap are read for its own live tiles.
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+template <class K>
+__device__ __forceinline__ f32x16 mfma_16x2(bf16x8 a, bf16x8 b, f32x16 c) {
+  f32x4v c0 = {c[0], c[1], c[2], c[3]}, c1 = {c[4], c[5], c[6], c[7]};
+  if constexpr (K::BF16) {
+    c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c1, 0, 0, 0);
+  } else {
+    c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c1, 0, 0, 0);
+  }
+  c[0] = c0[0]; c[1] = c0[1]; c[2] = c0[2]; c[3] = c0[3];
+  c[4] = c1[0]; c[5] = c1[1]; c[6] = c1[2]; c[7] = c1[3];
+  return c;
+}
+
 template <class K, int KK, int DEPTH, int MG_, int TAP>
 __device__ __forceinline__ void conv_tap_x(const char *src, const Nbr<K> &nb, f32x16 (&acc)[K::MT][K::NT],
                                            bf16x8 (&bc)[K::NT], bf16x8 (&bn)[K::NT], int (&off_cur)[K::NT],
@@ -688,7 +704,16 @@ __device__ __forceinline__ void conv_tap_x(const char *src, const Nbr<K> &nb, f3
       for (int m = 0; m < K::MT; ++m)
         a[slot][m] = wb.template load<WAUX>(wn_off + m * MSTRIDE + (uint32_t)(sn - STEPS) * 1024u);
     }
-    if constexpr (K::ABL & 4194304) {
+    if constexpr (K::ABL & 8388608) {
+      // timing ablation (wrong results): each 32x32x16 MFMA replaced by two 16x16x32 MFMAs on the same
+      // operands into two quarters of the accumulator (the same FLOPs, cycles and operand traffic) -- a
+      // probe of the MFMA-shape clock lever (MI355X_MICROARCH.md 'DVFS give-back' item 7) in this kernel
+#pragma unroll
+      for (int t = 0; t < K::NT; ++t)
+#pragma unroll
+        for (int m = 0; m < K::MT; ++m)
+          if ((LV >> t) & 1u) acc[m][t] = mfma_16x2<K>(acur[m], bc[t], acc[m][t]);
+    } else if constexpr (K::ABL & 4194304) {
       // A/B: weight-major MFMA order (the same A operand for NTA consecutive MFMAs; each accumulator's
       // k order is unchanged, so the outputs are bit-identical) -- an operand-toggling / clock probe
 #pragma unroll
@@ -1041,7 +1066,7 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
     const int wn_steps = L + 1 < n_convs ? LSTEPS : 0;
     if constexpr (K::XMAJ) {
       static_assert(K::ONEBUF || ((K::MG == 2 || (K::MG == 1 && K::EDGE)) &&
-                        (K::ABL & ~(2 | 4 | 8 | 16 | 128 | 512 | 4096 | 8192 | 16384 | 4194304)) == 0 && (K::ABL == 0 || K::EDGE)),
+                        (K::ABL & ~(2 | 4 | 8 | 16 | 128 | 512 | 4096 | 8192 | 16384 | 4194304 | 8388608)) == 0 && (K::ABL == 0 || K::EDGE)),
                     "column-group conv: two row halves (edge tiles: or one); edge tiles take the 2/4/8/16/128 timing ablations");
       const bool even = (L & 1) == 0;
       if constexpr (K::MG == 1) {
@@ -1694,6 +1719,8 @@ static int forward_ab(int32_t width, int32_t height, int32_t channels, int32_t n
       case 301: return launch<Cfg<128, 256, 7, 6, 2, 4, 4096, 4, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       // weight-major MFMA order within a k-step (bit-identical; clock / operand-toggling probe)
       case 304: return launch<Cfg<128, 256, 7, 6, 2, 4, 4194304, 4, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      // timing ablation (wrong results): two 16x16x32 MFMAs per 32x32x16 (the MFMA-shape clock probe)
+      case 308: return launch<Cfg<128, 256, 7, 6, 2, 4, 8388608, 4, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       case 302: return launch<Cfg<128, 256, 7, 6, 2, 4, 8192, 4, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       case 316: return launch<Cfg<128, 256, 7, 6, 2, 4, 16384, 4, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
 #undef ABLATE_EDGE
