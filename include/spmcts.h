@@ -288,6 +288,16 @@ int spmcts_tower_heads(int32_t width, int32_t height, int32_t channels, int32_t 
 int spmcts_head_epilogue(int32_t hidden, int32_t actions, const void *z_dev, int32_t ldz, int32_t batch,
                          const float *head_b_dev, float *probs_dev, float *values_dev, spmcts_stream stream);
 int spmcts_tower_supported(int32_t width, int32_t height, int32_t channels);
+/* The packed weight blob layout the trunk of this shape expects (replaces nothing in the reference: the
+ * blob is this library's own format, built by evaluator.HipTowerEvaluator.refresh from the module's
+ * state_dict, modules.py:88-107).  SPMCTS_WLAYOUT_32X32: every conv as [Cout/32][taps][Cin/16][64 lanes][8],
+ * block and head convs' input channels in the phys_off order.  SPMCTS_WLAYOUT_M16 (the 7x6 C = 128 trunk,
+ * tower_m16.h): the stem as 32X32; the block convs as [Cout/16][taps][Cin/32][64 lanes][8] (lane 16q + n:
+ * output channel 16 ct + n, input channels 32 k + 8 q ..) and the block and head convs' input channels in
+ * the phys16 order.  Returns -2 for an unsupported shape. */
+#define SPMCTS_WLAYOUT_32X32 0
+#define SPMCTS_WLAYOUT_M16 1
+int spmcts_tower_weight_layout(int32_t width, int32_t height, int32_t channels);
 /* Device-count variants: the batch size is read from count_dev (e.g. the leaf-row count written by
  * spmcts_select) so no host synchronisation is needed; max_batch bounds the grid.
  * flags: SPMCTS_TOWER_PACK = the launch shares the chip with concurrent launches on other streams

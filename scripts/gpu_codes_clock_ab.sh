@@ -14,7 +14,7 @@ for c in $CODES; do
   echo "outputs $c vs 200: $(python3 scripts/tower_code_equal.py cmp $O/c200.npz $O/c$c.npz)" | tee -a $O/summary.txt
 done
 for c in 200 $CODES; do
-  SPMCTS_LIB=$AB SPMCTS_TOWER_CG=$c timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES --kernel-include-regex "k_tower" -f csv -d $O/p_$c -o run -- \
+  SPMCTS_LIB=$AB SPMCTS_TOWER_CG=$c timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA --kernel-include-regex "k_tower" -f csv -d $O/p_$c -o run -- \
     python3 scripts/bench_tower.py --trunk-only --iters 10 --batch 6144 > $O/p.json 2> $O/p.err
   rc=$?; if [ $rc -ne 0 ]; then echo "pmc rc=$rc"; tail -5 $O/p.err; exit $rc; fi
   python3 scripts/tower_util.py $O/p_$c/run_counter_collection.csv $O/util_$c.json

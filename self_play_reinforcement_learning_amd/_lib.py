@@ -16,6 +16,7 @@ RNG_PHILOX, RNG_TAPE = 0, 1
 TOWER_PACK = 1  # spmcts_tower_forward_dev flags (include/spmcts.h SPMCTS_TOWER_PACK)
 TOWER_F16 = 2  # fp16 weights / activations / head features (include/spmcts.h SPMCTS_TOWER_F16)
 LEAF_F32, LEAF_F16, LEAF_BF16, LEAF_BOARD_I64 = 0, 1, 2, 3
+WLAYOUT_32X32, WLAYOUT_M16 = 0, 1  # spmcts_tower_weight_layout (include/spmcts.h SPMCTS_WLAYOUT_*)
 NCHW, NHWC = 0, 1
 PLAYER_MCTS, PLAYER_RANDOM, PLAYER_LOOKAHEAD = 0, 1, 2
 
@@ -126,6 +127,7 @@ _SIGS = {
     "spmcts_copy_probe": [_P, _P, _U64, _P],
     "spmcts_tower_forward": [_I32, _I32, _I32, _I32, _P, _I32, _P, _P, _P, _I32, _P],
     "spmcts_tower_supported": [_I32, _I32, _I32],
+    "spmcts_tower_weight_layout": [_I32, _I32, _I32],
     "spmcts_tower_heads": [_I32, _I32, _I32, _I32, _P, _I32, _P, _P, _P, _P, _I32, _P],
     "spmcts_head_epilogue": [_I32, _I32, _P, _I32, _I32, _P, _P, _P, _P],
     "spmcts_tower_forward_dev": [_I32, _I32, _I32, _I32, _P, _P, _I32, _P, _P, _P, _I32, _P],

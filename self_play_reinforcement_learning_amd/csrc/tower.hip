@@ -58,6 +58,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef short i16x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
 // Element type of the weights, the LDS activations and the head features: bf16, or fp16 = the
@@ -104,8 +105,10 @@ struct Ty<_Float16> {
 
 
 template <int C_, int ROWS_, int W_, int H_, int CG_ = 2, int WAVES_ = 4, int ABL_ = 0, int DEPTH_ = 4, int OCC_ = 1,
-          bool XMAJ_ = false, bool EDGE_ = false, class E_ = __bf16, bool ONEBUF_ = false>
+          bool XMAJ_ = false, bool EDGE_ = false, class E_ = __bf16, bool ONEBUF_ = false, bool M16_ = false>
 struct Cfg : Ty<E_> {
+  // M16 (tower_m16.h): the block convs on v_mfma_f32_16x16x32 with the phys16 channel order
+  static constexpr bool M16 = M16_;
   using E = E_;  // operand / activation element type (Ty)
   static constexpr int OCC = OCC_;  // resident workgroups per CU the register budget is sized for
   static constexpr int DEPTH = DEPTH_;  // weight-fragment prefetch distance (k-steps)
@@ -632,11 +635,12 @@ template <class K>
 __device__ __forceinline__ f32x16 mfma_16x2(bf16x8 a, bf16x8 b, f32x16 c) {
   f32x4v c0 = {c[0], c[1], c[2], c[3]}, c1 = {c[4], c[5], c[6], c[7]};
   if constexpr (K::BF16) {
+    // (the second with A and B swapped: with identical operands hipcc emitted only one of the two)
     c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c0, 0, 0, 0);
-    c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c1, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, c1, 0, 0, 0);
   } else {
     c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c0, 0, 0, 0);
-    c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c1, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, b), __builtin_bit_cast(f16x8, a), c1, 0, 0, 0);
   }
   c[0] = c0[0]; c[1] = c0[1]; c[2] = c0[2]; c[3] = c0[3];
   c[4] = c1[0]; c[5] = c1[1]; c[6] = c1[2]; c[7] = c1[3];
@@ -712,7 +716,7 @@ __device__ __forceinline__ void conv_tap_x(const char *src, const Nbr<K> &nb, f3
       for (int t = 0; t < K::NT; ++t)
 #pragma unroll
         for (int m = 0; m < K::MT; ++m)
-          if ((LV >> t) & 1u) acc[m][t] = mfma_16x2<K>(acur[m], bc[t], acc[m][t]);
+          if ((LV >> t) & 1u) acc[m][t] = mfma_16x2<K>(acur[m], bc[t], (TAP == 0 && kk == 0) ? f32x16{} : acc[m][t]);
     } else if constexpr (K::ABL & 4194304) {
       // A/B: weight-major MFMA order (the same A operand for NTA consecutive MFMAs; each accumulator's
       // k order is unchanged, so the outputs are bit-identical) -- an operand-toggling / clock probe
@@ -989,12 +993,17 @@ __device__ __forceinline__ void head_layer(const char *src, const bf16x8 *w, con
 // bias: stem C, blocks 2*C each, head C/2.
 // One workgroup's tile: boards [board0, board0 + BOARDS) of the batch (board < batch), all layers.
 #include "tower_wide.h"
+#include "tower_m16.h"
 
 template <class K>
 __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int batch, int board0, int n_blocks,
                                            const bf16x8 *wpk, const float *bias, uint16_t *out, uint4 *scr) {
   if constexpr (K::ONEBUF) {
     wide::tile<K>(smem, planes, batch, board0, n_blocks, wpk, bias, out, scr + blockIdx.x * (wide::Scr<K>::PER_WG / 16));
+    return;
+  }
+  if constexpr (K::M16) {
+    m16::tile<K>(smem, planes, batch, board0, n_blocks, wpk, bias, out);
     return;
   }
   char *X = smem;
@@ -1586,9 +1595,16 @@ static bool heads_co() {  // SPMCTS_HEADS=lds: the LDS-staged linear heads
   static const bool v = !env_is("SPMCTS_HEADS", "lds");
   return v;
 }
+// SPMCTS_TOWER_M16=0: the 32x32x16 C = 128 Connect4 trunk (round 3's kernel set, its weight layout); the
+// ring trunk and the SPMCTS_TOWER_CG variants take that layout too
+static bool m16_trunk() {
+  static const bool v = !env_is("SPMCTS_TOWER_M16", "0") && !getenv("SPMCTS_TOWER_RING") && !getenv("SPMCTS_TOWER_CG");
+  return v;
+}
 #else
 // The product library has exactly one kernel per (shape, dtype) and reads no switch; a switch of the
 // A/B library set in the environment is refused (SPMCTS_ERR_AB_SWITCH) rather than silently ignored.
+static constexpr bool m16_trunk() { return true; }
 static constexpr bool c256_board3() { return false; }
 static constexpr bool wide_tails3() { return false; }
 static constexpr bool heads_co256() { return true; }
@@ -1601,7 +1617,7 @@ static int ab_switch_guard() {
 #else
   static const int rc = [] {
     for (const char *n : {"SPMCTS_TOWER_CG", "SPMCTS_TOWER_RING", "SPMCTS_TOWER_C256", "SPMCTS_WIDE_TAILS", "SPMCTS_HEADS",
-                          "SPMCTS_HEADS_C256", "SPMCTS_TREE_BLOCK", "SPMCTS_EXPAND_CO"})
+                          "SPMCTS_HEADS_C256", "SPMCTS_TREE_BLOCK", "SPMCTS_EXPAND_CO", "SPMCTS_TOWER_M16"})
       if (getenv(n)) return SPMCTS_ERR_AB_SWITCH;
     return 0;
   }();
@@ -1614,10 +1630,17 @@ template <class E>
 static int forward_dev(int32_t width, int32_t height, int32_t channels, int32_t n_blocks, const void *planes_dev,
                        const int32_t *count_dev, int32_t max_batch, const void *weights_dev, const float *bias_dev,
                        void *features_dev, bool pack, hipStream_t s) {
-  if (width == 7 && height == 6 && channels == 128)
-    return launch_dyn<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true, true, E>, Cfg<128, 192, 7, 6, 2, 4, 0, 4, 1, false, false, E>,
-                      Cfg<128, 128, 7, 6, 2, 4, 0, 4, 1, false, false, E>>(planes_dev, count_dev, max_batch, n_blocks,
-                                                                          weights_dev, bias_dev, features_dev, pack, s);
+  if (width == 7 && height == 6 && channels == 128) {
+#ifdef SPMCTS_AB
+    if (!m16_trunk())  // round 3's 32x32x16 set: 6-board edge tiles + 4- / 3-board board-major tails
+      return launch_dyn<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true, true, E>, Cfg<128, 192, 7, 6, 2, 4, 0, 4, 1, false, false, E>,
+                        Cfg<128, 128, 7, 6, 2, 4, 0, 4, 1, false, false, E>>(planes_dev, count_dev, max_batch, n_blocks,
+                                                                            weights_dev, bias_dev, features_dev, pack, s);
+#endif
+    // 16x16x32 edge tiles for every board, tails included (tower_m16.h)
+    using KM = Cfg<128, 256, 7, 6, 2, 4, 0, 2, 1, true, true, E, false, true>;
+    return launch_dyn<KM, KM, KM>(planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, pack, s);
+  }
   if (width == 7 && height == 6 && channels == 256) {
     // 6-board one-buffer edge tiles (tower_wide.h) with 3-board tails
     using K3 = Cfg<256, 128, 7, 6, 4, 4, 0, 4, 1, false, false, E>;
@@ -1649,9 +1672,15 @@ static int forward_dev(int32_t width, int32_t height, int32_t channels, int32_t 
 template <class E>
 static int forward_host(int32_t width, int32_t height, int32_t channels, int32_t n_blocks, const char *pl, int32_t batch,
                         const void *weights_dev, const float *bias_dev, char *ft, hipStream_t s) {
-  if (width == 7 && height == 6 && channels == 128)
-    return launch_split<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true, true, E>, Cfg<128, 192, 7, 6, 2, 4, 0, 4, 1, false, false, E>,
-                        Cfg<128, 128, 7, 6, 2, 4, 0, 4, 1, false, false, E>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+  if (width == 7 && height == 6 && channels == 128) {
+#ifdef SPMCTS_AB
+    if (!m16_trunk())
+      return launch_split<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true, true, E>, Cfg<128, 192, 7, 6, 2, 4, 0, 4, 1, false, false, E>,
+                          Cfg<128, 128, 7, 6, 2, 4, 0, 4, 1, false, false, E>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+#endif
+    using KM = Cfg<128, 256, 7, 6, 2, 4, 0, 2, 1, true, true, E, false, true>;
+    return launch<KM>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+  }
   if (width == 7 && height == 6 && channels == 256) {
     using K3 = Cfg<256, 128, 7, 6, 4, 4, 0, 4, 1, false, false, E>;
 #ifdef SPMCTS_AB
@@ -1884,4 +1913,10 @@ extern "C" int spmcts_head_epilogue(int32_t hidden, int32_t actions, const void 
 
 extern "C" int spmcts_tower_supported(int32_t width, int32_t height, int32_t channels) {
   return ((width == 7 && height == 6) || (width == 3 && height == 3)) && (channels == 128 || channels == 256);
+}
+
+extern "C" int spmcts_tower_weight_layout(int32_t width, int32_t height, int32_t channels) {
+  using namespace tower;
+  if (!spmcts_tower_supported(width, height, channels)) return -2;
+  return (width == 7 && height == 6 && channels == 128 && m16_trunk()) ? SPMCTS_WLAYOUT_M16 : SPMCTS_WLAYOUT_32X32;
 }

@@ -194,13 +194,35 @@ def phys_channel_order(c):
     return (p - w) + 8 * ((w % 16) // 4) + 4 * (w // 16) + w % 4
 
 
-def _pack_conv(w, cin_pad=None, in_perm=False, dtype=torch.bfloat16):
+def phys_channel_order_m16(c):
+    """The phys16 order of the 16x16x32 trunk (csrc/tower_m16.h): within every 64-channel half, physical
+    position 16 q + 4 m + r holds output channel 16 m + 4 q + r (a lane's four 16-channel tiles' values
+    of one cell are one contiguous run).  The map swaps q and m, so it is its own inverse."""
+    p = torch.arange(c)
+    w = p % 64
+    return (p - w) + 16 * ((w % 16) // 4) + 4 * (w // 16) + w % 4
+
+
+def _pack_conv_m16(w, dtype=torch.bfloat16):
+    """A block conv for the 16x16x32 trunk (csrc/tower_m16.h): [Cout][Cin][3][3] -> fragments
+    [Cout/16][taps][Cin/32][64 lanes][8], lane 16 q + n holding W[16 ct + n][tap][physical input channels
+    32 k + 8 q .. + 8] (the input channel axis in the phys16 order of the layer that wrote them)."""
+    cout, cin, kh, kw = w.shape
+    w = w[:, phys_channel_order_m16(cin).to(w.device)]
+    taps = kh * kw
+    w = w.permute(0, 2, 3, 1).reshape(cout, taps, cin)               # [o][tap][c]
+    w = w.reshape(cout // 16, 16, taps, cin // 32, 4, 8)             # o = ct*16 + n ; c = k*32 + q*8 + j
+    w = w.permute(0, 2, 3, 4, 1, 5)                                  # [ct][tap][k][q][n][j] -> lane = q*16 + n
+    return w.reshape(-1).to(dtype)
+
+
+def _pack_conv(w, cin_pad=None, in_perm=False, dtype=torch.bfloat16, order=None):
     """[Cout][Cin][kh][kw] fp -> bf16 / fp16 fragments [Cout/32][taps][Cin/16][64 lanes][8] (csrc/tower.hip).
     in_perm: the layer reads activations another tower layer wrote, which sit in the physical channel
     order (phys_channel_order), so the input-channel axis is permuted to match."""
     cout, cin, kh, kw = w.shape
     if in_perm:
-        w = w[:, phys_channel_order(cin).to(w.device)]
+        w = w[:, (order or phys_channel_order)(cin).to(w.device)]
     if cin_pad is not None and cin_pad > cin:
         w = torch.cat([w, torch.zeros(cout, cin_pad - cin, kh, kw, dtype=w.dtype, device=w.device)], 1)
         cin = cin_pad
@@ -281,16 +303,20 @@ class HipTowerEvaluator(Evaluator):
         ws, bs = [], []
         w, b = fold(t.conv1, t.bn1)
         dt = self.dtype
+        # the blob layout the library's trunk for this shape expects (include/spmcts.h SPMCTS_WLAYOUT_*)
+        self.wlayout = self._lib.lib().spmcts_tower_weight_layout(self.W, self.H, self.C)
+        m16 = self.wlayout == self._lib.WLAYOUT_M16
         ws.append(_pack_conv(w, cin_pad=16, dtype=dt))
         bs.append(b)
         for blk in t.residual_blocks:
             for conv, bn in ((blk.conv1, blk.bn1), (blk.conv2, blk.bn2)):
                 w, b = fold(conv, bn)
-                ws.append(_pack_conv(w, in_perm=True, dtype=dt))
+                ws.append(_pack_conv_m16(w, dtype=dt) if m16 else _pack_conv(w, in_perm=True, dtype=dt))
                 bs.append(b)
         wp, bp = fold(t.conv_policy, t.policy_bn)
         wv, bv = fold(t.conv_value, t.value_bn)
-        ws.append(_pack_conv(torch.cat([wp, wv], 0), in_perm=True, dtype=dt))
+        ws.append(_pack_conv(torch.cat([wp, wv], 0), in_perm=True, dtype=dt,
+                             order=phys_channel_order_m16 if m16 else phys_channel_order))
         bs.append(torch.cat([bp, bv], 0))
         self.n_blocks = len(t.residual_blocks)
         self.wblob = torch.cat(ws).to(dev).contiguous()
