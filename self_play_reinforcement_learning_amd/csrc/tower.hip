@@ -1074,7 +1074,7 @@ __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int
     }
     const int wn_steps = L + 1 < n_convs ? LSTEPS : 0;
     if constexpr (K::XMAJ) {
-      static_assert(K::ONEBUF || ((K::MG == 2 || (K::MG == 1 && K::EDGE)) &&
+      static_assert(K::M16 || K::ONEBUF || ((K::MG == 2 || (K::MG == 1 && K::EDGE)) &&
                         (K::ABL & ~(2 | 4 | 8 | 16 | 128 | 512 | 4096 | 8192 | 16384 | 4194304 | 8388608)) == 0 && (K::ABL == 0 || K::EDGE)),
                     "column-group conv: two row halves (edge tiles: or one); edge tiles take the 2/4/8/16/128 timing ablations");
       const bool even = (L & 1) == 0;
@@ -1598,7 +1598,10 @@ static bool heads_co() {  // SPMCTS_HEADS=lds: the LDS-staged linear heads
 // SPMCTS_TOWER_M16=0: the 32x32x16 C = 128 Connect4 trunk (round 3's kernel set, its weight layout); the
 // ring trunk and the SPMCTS_TOWER_CG variants take that layout too
 static bool m16_trunk() {
-  static const bool v = !env_is("SPMCTS_TOWER_M16", "0") && !getenv("SPMCTS_TOWER_RING") && !getenv("SPMCTS_TOWER_CG");
+  // SPMCTS_TOWER_CG codes 16xx are variants of the 16x16x32 trunk (its weight layout)
+  static const bool cg16 = getenv("SPMCTS_TOWER_CG") && atoi(getenv("SPMCTS_TOWER_CG")) / 100 == 16;
+  static const bool v =
+      !env_is("SPMCTS_TOWER_M16", "0") && !getenv("SPMCTS_TOWER_RING") && (!getenv("SPMCTS_TOWER_CG") || cg16);
   return v;
 }
 #else
@@ -1748,6 +1751,11 @@ static int forward_ab(int32_t width, int32_t height, int32_t channels, int32_t n
       case 301: return launch<Cfg<128, 256, 7, 6, 2, 4, 4096, 4, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       // weight-major MFMA order within a k-step (bit-identical; clock / operand-toggling probe)
       case 304: return launch<Cfg<128, 256, 7, 6, 2, 4, 4194304, 4, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      // the 16x16x32 trunk (tower_m16.h, the default: DEPTH 2, grouped schedule) variants: weight ring 4 deep
+      // (1604), the compiler's own schedule (1600)
+      case 1604: return launch<Cfg<128, 256, 7, 6, 2, 4, 0, 4, 1, true, true, __bf16, false, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      case 1600: return launch<Cfg<128, 256, 7, 6, 2, 4, 256, 2, 1, true, true, __bf16, false, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      case 1602: return launch<Cfg<128, 256, 7, 6, 2, 4, 0, 2, 1, true, true, __bf16, false, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       // timing ablation (wrong results): two 16x16x32 MFMAs per 32x32x16 (the MFMA-shape clock probe)
       case 308: return launch<Cfg<128, 256, 7, 6, 2, 4, 8388608, 4, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       case 302: return launch<Cfg<128, 256, 7, 6, 2, 4, 8192, 4, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);

@@ -104,6 +104,8 @@ __device__ __forceinline__ void conv_tap(const char *src, const Nbr<K> &nb, f32x
           if ((LV >> t) & 1u)
             acc[mm][t][h] = mfma16<K>(acur[mm], bc[t][h], (TAP == 0 && k == 0) ? f32x4{} : acc[mm][t][h]);
     // one operand read or weight load per MFMA gap: 2 NTA LDS reads and 4 weight loads among 8 NTA MFMAs
+    // (A/B: Cfg ABL 256 leaves the order to the compiler)
+    if constexpr (!(K::ABL & 256)) {
 #pragma unroll
     for (int i = 0; i < 2 * NTA; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
@@ -115,6 +117,7 @@ __device__ __forceinline__ void conv_tap(const char *src, const Nbr<K> &nb, f32x
       __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
     }
     __builtin_amdgcn_sched_group_barrier(0x008, 8 * NTA - 2 * NTA - 4, 0);
+    }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = 0; t < K::NT; ++t) {
