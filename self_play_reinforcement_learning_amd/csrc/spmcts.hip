@@ -1070,14 +1070,21 @@ __global__ __launch_bounds__(256) void k_dedup_alias(View v) {
   if (s != t) v.srow[t] = v.srow[s];
 }
 
-__global__ __launch_bounds__(1024) void k_scan_need(View v, int32_t *count_out) {
+// 256 threads = one wave per SIMD: the kernel runs while the other lane's trunk holds every CU, in the
+// registers a trunk wave leaves free on its SIMD (512 - 424 = 88 per lane beside the C = 128 trunk; a
+// 1,024-thread block needs 4 x 24 there and waited for a trunk workgroup to retire: 37 -> 90 us average
+// in the bench trace, profiles/r04_bench_prof/)
+constexpr int SCAN_THREADS = 256;
+constexpr int SCAN_WAVES = SCAN_THREADS / 64;
+
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_need(View v, int32_t *count_out) {
   // wave totals of the two segments' owner counts (a two-level scan: 6 shuffle steps within each wave,
-  // 4 over the 16 wave totals, 2 barriers; the round-3 1,024-entry Hillis-Steele scan took 20 barriers
-  // and 8 KB of LDS, and ran 30-40 us beside a trunk workgroup whose waves hold the SIMDs' issue slots)
-  __shared__ int32_t s_w0[16], s_w1[16];
+  // 2 over the 4 wave totals, 2 barriers; the round-3 1,024-entry Hillis-Steele scan took 20 barriers
+  // and 8 KB of LDS)
+  __shared__ int32_t s_w0[SCAN_WAVES], s_w1[SCAN_WAVES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T = v.NS;  // pending slots (tree * K + j), tree order then in-flight order
-  const int chunk = (T + 1023) / 1024;
+  const int chunk = (T + SCAN_THREADS - 1) / SCAN_THREADS;
   const int lo = min(T, tid * chunk), hi = min(T, lo + chunk);
   int c0 = 0, c1 = 0;
   // unrolled so each thread's chunk of flags is fetched in one round of independent loads
@@ -1102,16 +1109,16 @@ __global__ __launch_bounds__(1024) void k_scan_need(View v, int32_t *count_out) 
   }
   __syncthreads();
   if (wave == 0) {
-    int w0 = lane < 16 ? s_w0[lane] : 0, w1 = lane < 16 ? s_w1[lane] : 0;
+    int w0 = lane < SCAN_WAVES ? s_w0[lane] : 0, w1 = lane < SCAN_WAVES ? s_w1[lane] : 0;
 #pragma unroll
-    for (int off = 1; off < 16; off <<= 1) {
+    for (int off = 1; off < SCAN_WAVES; off <<= 1) {
       const int a0 = __shfl_up(w0, off, 64), a1 = __shfl_up(w1, off, 64);
       if (lane >= off) {
         w0 += a0;
         w1 += a1;
       }
     }
-    if (lane < 16) {
+    if (lane < SCAN_WAVES) {
       s_w0[lane] = w0;
       s_w1[lane] = w1;
     }
@@ -1127,7 +1134,7 @@ __global__ __launch_bounds__(1024) void k_scan_need(View v, int32_t *count_out) 
       v.row_tree[r] = t;
       if (v.K > 1) v.srow[t] = r;
     }
-  if (tid == 1023) {  // the last thread's inclusive prefix is each segment's total
+  if (tid == SCAN_THREADS - 1) {  // the last thread's inclusive prefix is each segment's total
     v.row_count[0] = i0;
     v.row_count[1] = i1;
     v.gcnt[10] += i0 + i1;  // network rows emitted (counters.nn_rows)
@@ -2298,7 +2305,7 @@ static int launch_rows(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_de
     DISPATCH(h, hipLaunchKernelGGL(k_dedup_insert<GG>, dim3(nblk(h->v.NS, 256)), dim3(256), 0, s, h->v));
     hipLaunchKernelGGL(k_dedup_owner, dim3(nblk(h->v.NS, 256)), dim3(256), 0, s, h->v);
   }
-  hipLaunchKernelGGL(k_scan_need, dim3(1), dim3(1024), 0, s, h->v, leaf_count_dev);
+  hipLaunchKernelGGL(k_scan_need, dim3(1), dim3(SCAN_THREADS), 0, s, h->v, leaf_count_dev);
   if (h->v.dedup) hipLaunchKernelGGL(k_dedup_alias, dim3(nblk(h->v.NS, 256)), dim3(256), 0, s, h->v);
   if (leaves_dev) {
     const long long total = (long long)h->v.NS * h->cells;

@@ -514,7 +514,7 @@ class _Trainer:
     GRAPH_WARMUP = 3
 
     def __init__(self, network, optim, memory_size, batch_size, min_memory, q_average, device, W=7, H=6, A=7,
-                 train_mode=True, overlap=True, autocast=False, graph=True):
+                 train_mode=True, overlap=True, autocast=False, graph=True, gemm_convs=True):
         from .replay import DeviceReplay
 
         dev = torch.device(device) if device is not None else torch.device("cpu")
@@ -536,6 +536,9 @@ class _Trainer:
         self.scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optim, "max", patience=15, factor=0.5,
                                                                     min_lr=0.00001, cooldown=5)
         self.graph = bool(graph) and dev.type == "cuda"
+        # ResidualTower networks on a CUDA device: the forward/backward in cell-major rows with every
+        # convolution one GEMM (modules.ResidualTower.forward_planes_rows; same function and parameters)
+        self.gemm_convs = bool(gemm_convs) and dev.type == "cuda" and hasattr(network, "forward_planes_rows")
         self._g = None          # the captured step (torch.cuda.CUDAGraph)
         self._g_key = None      # (lr of every param group, autocast, train_mode) it was captured with
         self._g_in = None       # its static inputs (s, z, pi, q)
@@ -572,16 +575,22 @@ class _Trainer:
 
     def _train_step(self, s, z, pi, q):
         self.network.train(self.train_mode)
+        self._rows(True)
         with torch.autocast("cuda", dtype=torch.float16, enabled=self.autocast):
             loss = az_loss(self.network, s, z, pi, q, self.q_average)
             self.optim.zero_grad()
             loss.backward()
             self.optim.step()
+        self._rows(False)
         self.network.eval()
         return loss.detach()
 
+    def _rows(self, on):
+        if self.gemm_convs:
+            self.network.gemm_convs = on
+
     def _graph_key(self):
-        return (tuple(float(g["lr"]) for g in self.optim.param_groups), self.autocast, self.train_mode)
+        return (tuple(float(g["lr"]) for g in self.optim.param_groups), self.autocast, self.train_mode, self.gemm_convs)
 
     def _step_graphed(self, s, z, pi, q):
         """One update through the captured graph (on the current stream).  The first GRAPH_WARMUP
@@ -611,11 +620,13 @@ class _Trainer:
         self.optim.zero_grad(set_to_none=True)  # the gradients are allocated inside the graph's pool
         # captured on torch's side stream (it synchronises the device once, here); replays run on the
         # caller's current stream
+        self._rows(True)
         with torch.cuda.graph(g):
             with torch.autocast("cuda", dtype=torch.float16, enabled=self.autocast, cache_enabled=False):
                 loss = az_loss(self.network, *self._g_in, self.q_average)
             loss.backward()
             self.optim.step()
+        self._rows(False)
         self.network.eval()
         self._g, self._g_loss = g, loss
         self.graph_captures += 1
