@@ -6,7 +6,7 @@ set -u
 O=gpurun_out/r04h
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 60 python3 scripts/diag/bn_rows.py && timeout -k 10 900 python -u -m pytest tests/test_gpu_engine.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_gpu_engine.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1
 rc=$?; tail -1 $O/tests.log; [ $rc -eq 0 ] || { grep -B5 -A30 "FAILED\|Error" $O/tests.log | head -60; exit $rc; }
 timeout -k 10 400 python3 scripts/bench_train.py --trainer-gemm-ab > $O/train_ab.json 2> $O/train_ab.err || { tail -5 $O/train_ab.err; exit 1; }
 python3 -c "

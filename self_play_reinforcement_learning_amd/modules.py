@@ -74,10 +74,16 @@ def _bn_rows(bn, y):
     if bn.training and bn.track_running_stats:
         bn.num_batches_tracked.add_(1)
     use_batch = bn.training or not bn.track_running_stats
-    # as [N, C, 1, 1]: the library's spatial (per-channel) kernels, as for BatchNorm2d; a 2-D [N, C] input
-    # takes MIOpen's per-activation path, which gave NaN on fp16 rows (scripts/diag/bn_rows.py)
-    out = F.batch_norm(y.reshape(-1, shape[-1], 1, 1), bn.running_mean, bn.running_var, bn.weight, bn.bias, use_batch,
-                       bn.momentum, bn.eps)
+    # PyTorch's own batch-norm kernels (channels-last reductions over the rows), not MIOpen's: MIOpen's
+    # train-mode kernels on [N, C] / [N, C, 1, 1] inputs gave NaN losses inside a captured HIP graph
+    # (eager steps were fine; scripts/diag/bn_rows.py, trainer_rows_nan.py)
+    prev = torch.backends.cudnn.enabled
+    torch.backends.cudnn.enabled = False
+    try:
+        out = F.batch_norm(y.reshape(-1, shape[-1]), bn.running_mean, bn.running_var, bn.weight, bn.bias, use_batch,
+                           bn.momentum, bn.eps)
+    finally:
+        torch.backends.cudnn.enabled = prev
     return out.view(shape)
 
 

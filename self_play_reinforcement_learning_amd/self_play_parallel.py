@@ -93,7 +93,8 @@ class SelfPlayScheduler:
                  save_dir="saves", epoch_length=500, initial_games=64, lr=0.001, stagger=False, evaluation_games=100,
                  evaluation_network=None, stagger_mem_step=5000, deduplicate=False, update_delay=0.01,
                  self_play=None, n_games=None, device=None, seed=0, updates_per_ply=4, lanes=None, exchange_every=8,
-                 gpus=None, start_time=None, overlap_training=False, train_autocast=True, train_graph=True):
+                 gpus=None, start_time=None, overlap_training=False, train_autocast=True, train_graph=True,
+                 train_gemm_convs=True):
         # constructor arguments, for rank processes started by this scheduler (_run_ranks)
         self._init_kwargs = {k: v for k, v in locals().items() if k not in ("self", "__class__")}
         self.policy_container = policy_container
@@ -125,6 +126,7 @@ class SelfPlayScheduler:
         self.train_autocast = train_autocast
         # the trainer's update captured as one HIP graph and replayed per step (_Trainer graph=True)
         self.train_graph = train_graph
+        self.train_gemm_convs = train_gemm_convs
         self.exchange_every = exchange_every  # plies per episode-batch exchange round (distributed.MoveExchange)
         # >1: LanedEngine (arenas on separate HIP streams, each a complete arena); None = 2 lanes for
         # arenas of >= 1,024 games, where the overlap pays (bench.py), else one arena
@@ -207,7 +209,7 @@ class SelfPlayScheduler:
                                 batch_size=kw.get("batch_size", 64), min_memory=kw.get("min_memory", 20000),
                                 q_average=kw.get("q_average", True), device=self.device, W=self.W, H=self.H,
                                 A=self.A, overlap=self._overlap_ok(), autocast=self.train_autocast,
-                                graph=self.train_graph)
+                                graph=self.train_graph, gemm_convs=self.train_gemm_convs)
         if resume_model:
             self._load_latest(prev_run=True)
         return self.trainer, None, None
