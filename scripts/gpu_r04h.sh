@@ -6,6 +6,8 @@ set -u
 O=gpurun_out/r04h
 mkdir -p $O
 export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_engine.py::test_trainer_graph_train_mode_replays_run -m gpu -x -q --timeout 120 --timeout-method thread > $O/one.log 2>&1; echo "one rc=$?"; grep "AssertionError" $O/one.log | head -3
+timeout -k 10 300 python -u -m pytest tests/test_gpu_engine.py::test_trainer_graph_train_mode_replays_run -m gpu -x -q > $O/one2.log 2>&1; echo "one (no timeout plugin) rc=$?"; grep "AssertionError" $O/one2.log | head -3
 timeout -k 10 900 python -u -m pytest tests/test_gpu_engine.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1
 rc=$?; tail -1 $O/tests.log; [ $rc -eq 0 ] || { grep -B5 -A30 "FAILED\|Error" $O/tests.log | head -60; exit $rc; }
 timeout -k 10 400 python3 scripts/bench_train.py --trainer-gemm-ab > $O/train_ab.json 2> $O/train_ab.err || { tail -5 $O/train_ab.err; exit 1; }
