@@ -63,7 +63,7 @@ def run(args, updates, overlap, autocast=True, graph=True):
                 replay_rows=len(tr.memory), last_loss=loss)
 
 
-def trainer_only(args, graph, autocast=True, steps=40, channels_last=False, benchmark=False, gemm_convs=True):
+def trainer_only(args, graph, autocast=True, steps=40, channels_last=False, benchmark=False):
     """ms per SGD step of the trainer alone (batch 64, ResNet-128x20, train mode), graphed or eager;
     `channels_last`: the network's tensors in NHWC order; `benchmark`: MIOpen's exhaustive kernel search
     (torch.backends.cudnn.benchmark)."""
@@ -79,7 +79,7 @@ def trainer_only(args, graph, autocast=True, steps=40, channels_last=False, benc
         net = net.to(memory_format=torch.channels_last)
     tr = _Trainer(net, torch.optim.SGD(net.parameters(), lr=0.001, momentum=0.9, weight_decay=1e-4), memory_size=200000,
                   batch_size=64, min_memory=0, q_average=True, device="cuda", overlap=True, autocast=autocast,
-                  graph=graph, gemm_convs=gemm_convs)
+                  graph=graph)
     g = torch.Generator().manual_seed(0)
     n = 20000
     tr.memory.add_moves(dict(state=torch.randint(-1, 2, (n, 42), dtype=torch.int8, generator=g),
@@ -96,8 +96,7 @@ def trainer_only(args, graph, autocast=True, steps=40, channels_last=False, benc
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     torch.backends.cudnn.benchmark = False
-    return dict(train_graph=graph, train_autocast=autocast, gemm_convs=gemm_convs, channels_last=channels_last,
-                benchmark=benchmark, steps=steps,
+    return dict(train_graph=graph, train_autocast=autocast, channels_last=channels_last, benchmark=benchmark, steps=steps,
                 ms_per_sgd_step=dt / steps * 1e3, graph_captures=tr.graph_captures, last_loss=float(tr.last_loss))
 
 
@@ -111,17 +110,9 @@ def main():
     ap.add_argument("--trainer-variants", action="store_true",
                     help="trainer-only timings of graphed steps with NHWC tensors and MIOpen's exhaustive search, "
                          "no self-play runs")
-    ap.add_argument("--trainer-gemm-ab", action="store_true",
-                    help="trainer-only timings with GEMM-form convolutions (the default) against the convolution "
-                         "library's, graphed and eager, fp16 autocast and fp32, each twice")
     ap.add_argument("--trainer-only-graph", action="store_true",
                     help="only the graphed fp16-autocast trainer-only timing (for a kernel trace)")
     args = ap.parse_args()
-    if args.trainer_gemm_ab:
-        rows = [trainer_only(args, g, autocast=a, gemm_convs=c) for g in (True, False) for a in (True, False)
-                for c in (True, False) for _ in range(2)]
-        print(json.dumps(dict(trainer_only=rows)), flush=True)
-        return
     if args.trainer_only_graph:
         print(json.dumps(dict(trainer_only=[trainer_only(args, True, steps=100)])), flush=True)
         return

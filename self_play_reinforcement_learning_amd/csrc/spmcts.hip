@@ -1070,16 +1070,16 @@ __global__ __launch_bounds__(256) void k_dedup_alias(View v) {
   if (s != t) v.srow[t] = v.srow[s];
 }
 
-// 256 threads = one wave per SIMD: the kernel runs while the other lane's trunk holds every CU, in the
+// 512 threads = two waves per SIMD: the kernel runs while the other lane's trunk holds every CU, in the
 // registers a trunk wave leaves free on its SIMD (512 - 424 = 88 per lane beside the C = 128 trunk; a
 // 1,024-thread block needs 4 x 24 there and waited for a trunk workgroup to retire: 37 -> 90 us average
-// in the bench trace, profiles/r04_bench_prof/)
-constexpr int SCAN_THREADS = 256;
+// in the bench trace, profiles/r04_bench_prof/; 256 threads: 64 us, two rounds of flag loads per pass)
+constexpr int SCAN_THREADS = 512;
 constexpr int SCAN_WAVES = SCAN_THREADS / 64;
 
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan_need(View v, int32_t *count_out) {
   // wave totals of the two segments' owner counts (a two-level scan: 6 shuffle steps within each wave,
-  // 2 over the 4 wave totals, 2 barriers; the round-3 1,024-entry Hillis-Steele scan took 20 barriers
+  // 3 over the 8 wave totals, 2 barriers; the round-3 1,024-entry Hillis-Steele scan took 20 barriers
   // and 8 KB of LDS)
   __shared__ int32_t s_w0[SCAN_WAVES], s_w1[SCAN_WAVES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;

@@ -59,34 +59,6 @@ def planes_from_boards(s, width, height):
     return torch.stack([(s == 0), (s == 1), (s == -1)], 1).float()
 
 
-def _conv3x3_rows(x, conv):
-    """3x3 / pad 1 / stride 1 convolution of channels-last rows x [B, W, H, C] -> [B, W, H, Cout]: im2col
-    (the [C, 3, 3] window of every cell, in the weight's own flattening order) and one GEMM."""
-    B, Wd, Hd, C = x.shape
-    cols = F.pad(x, (0, 0, 1, 1, 1, 1)).unfold(1, 3, 1).unfold(2, 3, 1)  # [B, W, H, C, 3, 3]
-    y = F.linear(cols.reshape(B * Wd * Hd, C * 9), conv.weight.flatten(1), conv.bias)
-    return y.view(B, Wd, Hd, -1)
-
-
-def _bn_rows(bn, y):
-    """BatchNorm2d.forward on channels-last rows: per-channel statistics over every leading index."""
-    shape = y.shape
-    if bn.training and bn.track_running_stats:
-        bn.num_batches_tracked.add_(1)
-    use_batch = bn.training or not bn.track_running_stats
-    # PyTorch's own batch-norm kernels (channels-last reductions over the rows), not MIOpen's: MIOpen's
-    # train-mode kernels on [N, C] / [N, C, 1, 1] inputs gave NaN losses inside a captured HIP graph
-    # (eager steps were fine; scripts/diag/bn_rows.py, trainer_rows_nan.py)
-    prev = torch.backends.cudnn.enabled
-    torch.backends.cudnn.enabled = False
-    try:
-        out = F.batch_norm(y.reshape(-1, shape[-1]), bn.running_mean, bn.running_var, bn.weight, bn.bias, use_batch,
-                           bn.momentum, bn.eps)
-    finally:
-        torch.backends.cudnn.enabled = prev
-    return out.view(shape)
-
-
 class ResidualTower(nn.Module):
     """ResidualTower(width, height, action_size, num_blocks, default_kernel_size, filter_factor)."""
 
@@ -125,46 +97,13 @@ class ResidualTower(nn.Module):
         """modules.py:75-77"""
         return ResidualTower(env.width, env.height, env.num_actions(), num_blocks, filter_factor=filter_factor)
 
-    # trainer-side option (self_play_parallel._Trainer(gemm_convs=True)): forward_planes runs the same
-    # network in cell-major rows, every convolution as one GEMM (forward_planes_rows)
-    gemm_convs = False
-
     def forward_planes(self, x):
-        if self.gemm_convs:
-            return self.forward_planes_rows(x)
         x = self.relu(self.bn1(self.conv1(x)))
         x = self.residual_blocks(x)
         policy = F.relu(self.policy_bn(self.conv_policy(x))).flatten(1)
         policy = self.softmax(self.linear_policy(self.policy_dropout(policy)))
         value = F.relu(self.value_bn(self.conv_value(x))).flatten(1)
         value = F.relu(self.fc_value(self.value_dropout(value)))
-        value = torch.tanh(self.linear_output(value))
-        return policy, value
-
-    def forward_planes_rows(self, x):
-        """forward_planes with the activations as cell-major rows [B*W*H, C] (channels last): every 3x3
-        convolution is one im2col copy + one GEMM with the bias in its epilogue (F.linear), its backward
-        two GEMMs + the im2col's adjoint; every BatchNorm normalises the rows per channel, over batch and
-        cells as BatchNorm2d does (same batch statistics, same running-statistics update); the heads'
-        features are flattened in the reference's [C, W, H] order for the Linear layers.  The same
-        parameters and the same function as forward_planes up to rounding (tests/test_train_rows.py);
-        for the trainer at batch 64, where the convolution library's 3x3 kernels run at a few % of the
-        chip (DESIGN.md §4 "Trainer step")."""
-        B, _, Wd, Hd = x.shape
-        rows = x.permute(0, 2, 3, 1)  # [B, W, H, 3]
-        rows = F.relu(_bn_rows(self.bn1, _conv3x3_rows(rows, self.conv1)))
-        for blk in self.residual_blocks:
-            y = F.relu(_bn_rows(blk.bn1, _conv3x3_rows(rows, blk.conv1)))
-            y = _bn_rows(blk.bn2, _conv3x3_rows(y, blk.conv2))
-            rows = F.relu(y + rows)
-        flat = rows.reshape(B * Wd * Hd, -1)
-
-        def head(conv, bn):
-            h = F.relu(_bn_rows(bn, F.linear(flat, conv.weight.flatten(1), conv.bias)))
-            return h.view(B, Wd * Hd, -1).transpose(1, 2).reshape(B, -1)  # [B, C*W*H] as flatten(1) of NCHW
-
-        policy = self.softmax(self.linear_policy(self.policy_dropout(head(self.conv_policy, self.policy_bn))))
-        value = F.relu(self.fc_value(self.value_dropout(head(self.conv_value, self.value_bn))))
         value = torch.tanh(self.linear_output(value))
         return policy, value
 

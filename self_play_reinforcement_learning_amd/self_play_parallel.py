@@ -93,8 +93,7 @@ class SelfPlayScheduler:
                  save_dir="saves", epoch_length=500, initial_games=64, lr=0.001, stagger=False, evaluation_games=100,
                  evaluation_network=None, stagger_mem_step=5000, deduplicate=False, update_delay=0.01,
                  self_play=None, n_games=None, device=None, seed=0, updates_per_ply=4, lanes=None, exchange_every=8,
-                 gpus=None, start_time=None, overlap_training=False, train_autocast=True, train_graph=True,
-                 train_gemm_convs=True):
+                 gpus=None, start_time=None, overlap_training=False, train_autocast=True, train_graph=True):
         # constructor arguments, for rank processes started by this scheduler (_run_ranks)
         self._init_kwargs = {k: v for k, v in locals().items() if k not in ("self", "__class__")}
         self.policy_container = policy_container
@@ -126,7 +125,6 @@ class SelfPlayScheduler:
         self.train_autocast = train_autocast
         # the trainer's update captured as one HIP graph and replayed per step (_Trainer graph=True)
         self.train_graph = train_graph
-        self.train_gemm_convs = train_gemm_convs
         self.exchange_every = exchange_every  # plies per episode-batch exchange round (distributed.MoveExchange)
         # >1: LanedEngine (arenas on separate HIP streams, each a complete arena); None = 2 lanes for
         # arenas of >= 1,024 games, where the overlap pays (bench.py), else one arena
@@ -209,7 +207,7 @@ class SelfPlayScheduler:
                                 batch_size=kw.get("batch_size", 64), min_memory=kw.get("min_memory", 20000),
                                 q_average=kw.get("q_average", True), device=self.device, W=self.W, H=self.H,
                                 A=self.A, overlap=self._overlap_ok(), autocast=self.train_autocast,
-                                graph=self.train_graph, gemm_convs=self.train_gemm_convs)
+                                graph=self.train_graph)
         if resume_model:
             self._load_latest(prev_run=True)
         return self.trainer, None, None
@@ -516,7 +514,7 @@ class _Trainer:
     GRAPH_WARMUP = 3
 
     def __init__(self, network, optim, memory_size, batch_size, min_memory, q_average, device, W=7, H=6, A=7,
-                 train_mode=True, overlap=True, autocast=False, graph=True, gemm_convs=True):
+                 train_mode=True, overlap=True, autocast=False, graph=True):
         from .replay import DeviceReplay
 
         dev = torch.device(device) if device is not None else torch.device("cpu")
@@ -538,9 +536,6 @@ class _Trainer:
         self.scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optim, "max", patience=15, factor=0.5,
                                                                     min_lr=0.00001, cooldown=5)
         self.graph = bool(graph) and dev.type == "cuda"
-        # ResidualTower networks on a CUDA device: the forward/backward in cell-major rows with every
-        # convolution one GEMM (modules.ResidualTower.forward_planes_rows; same function and parameters)
-        self.gemm_convs = bool(gemm_convs) and dev.type == "cuda" and hasattr(network, "forward_planes_rows")
         self._g = None          # the captured step (torch.cuda.CUDAGraph)
         self._g_key = None      # (lr of every param group, autocast, train_mode) it was captured with
         self._g_in = None       # its static inputs (s, z, pi, q)
@@ -577,22 +572,16 @@ class _Trainer:
 
     def _train_step(self, s, z, pi, q):
         self.network.train(self.train_mode)
-        self._rows(True)
         with torch.autocast("cuda", dtype=torch.float16, enabled=self.autocast):
             loss = az_loss(self.network, s, z, pi, q, self.q_average)
             self.optim.zero_grad()
             loss.backward()
             self.optim.step()
-        self._rows(False)
         self.network.eval()
         return loss.detach()
 
-    def _rows(self, on):
-        if self.gemm_convs:
-            self.network.gemm_convs = on
-
     def _graph_key(self):
-        return (tuple(float(g["lr"]) for g in self.optim.param_groups), self.autocast, self.train_mode, self.gemm_convs)
+        return (tuple(float(g["lr"]) for g in self.optim.param_groups), self.autocast, self.train_mode)
 
     def _step_graphed(self, s, z, pi, q):
         """One update through the captured graph (on the current stream).  The first GRAPH_WARMUP
@@ -622,13 +611,11 @@ class _Trainer:
         self.optim.zero_grad(set_to_none=True)  # the gradients are allocated inside the graph's pool
         # captured on torch's side stream (it synchronises the device once, here); replays run on the
         # caller's current stream
-        self._rows(True)
         with torch.cuda.graph(g):
             with torch.autocast("cuda", dtype=torch.float16, enabled=self.autocast, cache_enabled=False):
                 loss = az_loss(self.network, *self._g_in, self.q_average)
             loss.backward()
             self.optim.step()
-        self._rows(False)
         self.network.eval()
         self._g, self._g_loss = g, loss
         self.graph_captures += 1
