@@ -110,20 +110,9 @@ def main():
     ap.add_argument("--trainer-variants", action="store_true",
                     help="trainer-only timings of graphed steps with NHWC tensors and MIOpen's exhaustive search, "
                          "no self-play runs")
-    ap.add_argument("--trainer-dtype-ab", action="store_true",
-                    help="trainer-only ms per SGD step under fp16 (the reference's) and bf16 autocast, graphed and "
-                         "eager, each twice")
     ap.add_argument("--trainer-only-graph", action="store_true",
                     help="only the graphed fp16-autocast trainer-only timing (for a kernel trace)")
     args = ap.parse_args()
-    if args.trainer_dtype_ab:
-        import torch
-
-        rows = [trainer_only(args, g, autocast=a) for g in (True, False) for a in (True, torch.bfloat16) for _ in range(2)]
-        for r in rows:
-            r["train_autocast"] = str(r["train_autocast"])
-        print(json.dumps(dict(trainer_only=rows)), flush=True)
-        return
     if args.trainer_only_graph:
         print(json.dumps(dict(trainer_only=[trainer_only(args, True, steps=100)])), flush=True)
         return

@@ -532,9 +532,7 @@ class _Trainer:
         # forward, loss and backward under fp16 autocast as the UpdateWorker (updateworker.py:147-149:
         # `with autocast(): self.policy.update_from_memory()`, no GradScaler); only on a CUDA device,
         # where the reference's autocast is active (it is a no-op on CPU)
-        # (`autocast=torch.bfloat16`: the same under bf16 autocast, an MI355X option, not the reference's)
         self.autocast = bool(autocast) and dev.type == "cuda"
-        self.autocast_dtype = autocast if isinstance(autocast, torch.dtype) else torch.float16
         self.scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optim, "max", patience=15, factor=0.5,
                                                                     min_lr=0.00001, cooldown=5)
         self.graph = bool(graph) and dev.type == "cuda"
@@ -574,7 +572,7 @@ class _Trainer:
 
     def _train_step(self, s, z, pi, q):
         self.network.train(self.train_mode)
-        with torch.autocast("cuda", dtype=self.autocast_dtype, enabled=self.autocast):
+        with torch.autocast("cuda", dtype=torch.float16, enabled=self.autocast):
             loss = az_loss(self.network, s, z, pi, q, self.q_average)
             self.optim.zero_grad()
             loss.backward()
@@ -583,8 +581,7 @@ class _Trainer:
         return loss.detach()
 
     def _graph_key(self):
-        return (tuple(float(g["lr"]) for g in self.optim.param_groups), self.autocast, self.autocast_dtype,
-                self.train_mode)
+        return (tuple(float(g["lr"]) for g in self.optim.param_groups), self.autocast, self.train_mode)
 
     def _step_graphed(self, s, z, pi, q):
         """One update through the captured graph (on the current stream).  The first GRAPH_WARMUP
@@ -615,7 +612,7 @@ class _Trainer:
         # captured on torch's side stream (it synchronises the device once, here); replays run on the
         # caller's current stream
         with torch.cuda.graph(g):
-            with torch.autocast("cuda", dtype=self.autocast_dtype, enabled=self.autocast, cache_enabled=False):
+            with torch.autocast("cuda", dtype=torch.float16, enabled=self.autocast, cache_enabled=False):
                 loss = az_loss(self.network, *self._g_in, self.q_average)
             loss.backward()
             self.optim.step()
