@@ -8,9 +8,10 @@
 // 32-row x 32-channel output tile computed as 2 x 2 tiles of 16 x 16 over K = 32 input channels per MFMA:
 //   * A (weights): fragment (16-channel tile, tap, 32-channel k-step), lane l = 16 q + n holds
 //     W[16 ct + n][tap][physical input channels 32 k + 8 q .. + 8] (evaluator._pack_conv_m16);
-//   * B (activations): lane l reads 16 bytes of row (tile t, half h, cell n = l & 15) at physical
-//     channels 32 k + 8 q: the same rows and bytes per k-step as the 32x32x16 form, other lane addresses;
-//   * D: lane l holds output channels 16 mm + 4 q + r (r = 0..3) of cell n; stored at the PHYSICAL
+//   * B (activations): lane l reads 16 bytes of row (tile t, row lane_row(l & 15) + h) at physical
+//     channels 32 k + 8 q: the same rows and bytes per k-step as the 32x32x16 form, other lane addresses
+//     (lane_row: the fragment's rows are the tile's rows of one residue parity, bank-conflict free);
+//   * D: lane l holds output channels 16 mm + 4 q + r (r = 0..3) of that row; stored at the PHYSICAL
 //     position 64 cg + 16 q + 4 mm + r (phys16), so each lane's 16 values of a cell are one contiguous
 //     32-byte run (the next layer's weights take their input channels in this order; it is its own
 //     inverse: evaluator.phys_channel_order_m16).
@@ -25,10 +26,28 @@ namespace m16 {
 // byte offset, within a row, of the physical 16-channel run of lane quarter q in channel half cg
 __device__ __forceinline__ int run_off(int cg, int q) { return (64 * cg + 16 * q) * 2; }
 
-// the source row of (tile t, 16-row half h) for `tap`: the edge table, for this lane's cell n
+// Which of a 32-row tile's rows MFMA column n of fragment h (0, 1) stands for: row lane_row(n) + h.
+// A B-fragment ds_read_b128 is serviced in 16-lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32)
+// (MI355X_MICROARCH.md §LDS); lane 16 q + n reads its row at 16-B slot (row + q + 4 k) mod 16 (272-B
+// rows), so group 0 holds columns A = {0-3, 12-15} at quarter q and B = {4-11} at q + 1, group 1 the
+// reverse.  With column n on row n (round 4) the two k offsets of a group collide (44 % of the trunk's LDS
+// cycles were conflict cycles, profiles/r04/m16/stall_lds_pmc.txt): no permutation of one 16-row half
+// avoids it (the A rows and the B rows + 1 would both have to fill the residues the other leaves).  Here
+// fragment h takes the tile's 16 rows of residue parity h, each residue once in A and once in B: A's
+// residues 2 i + h and B's 2 i + h + 1 are disjoint, so every group reads 16 distinct slots at the
+// centre tap, and — the edge rows are residue-coloured (tower_edge.h: a tap shifts every row's residue
+// by the same amount) — at every tap (tests/test_tower_edge_layout.py checks all 60 live (tile, tap)
+// reads).  Each output element is the same MFMA sum as before, only in another column: bit-identical.
+__device__ __forceinline__ int lane_row(int n) {
+  const bool in_a = n < 4 || n >= 12;
+  const int i = in_a ? (n < 4 ? n : n - 8) : n - 4;
+  return (in_a ? 0 : 16) + 2 * i;
+}
+
+// the source row of (tile t, fragment h) for `tap`: the edge table, for this lane's row rb + h
 template <class K>
-__device__ __forceinline__ int src_row(const Nbr<K> &nb, int mg, int t, int h, int n, int tap) {
-  return (int)nb.tab[tap * K::ROWS + (mg * K::NT + t) * 32 + 16 * h + n];
+__device__ __forceinline__ int src_row(const Nbr<K> &nb, int mg, int t, int h, int rb, int tap) {
+  return (int)nb.tab[tap * K::ROWS + (mg * K::NT + t) * 32 + rb + h];
 }
 
 template <class K>
@@ -45,7 +64,7 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 template <class K, int KK32, int DEPTH, int MG_, int TAP>
 __device__ __forceinline__ void conv_tap(const char *src, const Nbr<K> &nb, f32x4 (&acc)[4][K::NT][2],
                                          bf16x8 (&bc)[K::NT][2], bf16x8 (&bn)[K::NT][2], int (&off_cur)[K::NT][2],
-                                         int (&off_nxt)[K::NT][2], bf16x8 (&a)[DEPTH][4], int qoff, int n,
+                                         int (&off_nxt)[K::NT][2], bf16x8 (&a)[DEPTH][4], int qoff, int rb,
                                          const WBuf &wb, uint32_t wl_off, uint32_t wn_off, int wn_steps) {
   using X = XLive<K, MG_>;
   constexpr uint32_t MSTRIDE = 9u * KK32 * 1024u;  // bytes between a wave's 16-channel tiles
@@ -58,8 +77,8 @@ __device__ __forceinline__ void conv_tap(const char *src, const Nbr<K> &nb, f32x
 #pragma unroll
     for (int t = 0; t < K::NT; ++t)
       if ((LVN >> t) & 1u) {
-        off_nxt[t][0] = src_row(nb, MG_, t, 0, n, TAP + 1);
-        off_nxt[t][1] = src_row(nb, MG_, t, 1, n, TAP + 1);
+        off_nxt[t][0] = src_row(nb, MG_, t, 0, rb, TAP + 1);
+        off_nxt[t][1] = src_row(nb, MG_, t, 1, rb, TAP + 1);
       }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -135,14 +154,14 @@ __device__ __forceinline__ void conv_tap(const char *src, const Nbr<K> &nb, f32x
 // out = relu(acc + bias (+ the block input at the same physical positions, RESID)), into dst.
 template <class K, bool RESID>
 __device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][K::NT][2], char *dst, const float4 (&bv)[4], int cg,
-                                         int mg, int q, int n) {
+                                         int mg, int q, int rb) {
 #pragma unroll
   for (int t = 0; t < K::NT; ++t) {
     uint4 res[2][2];
     if constexpr (RESID) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const char *p = dst + ((mg * K::NT + t) * 32 + 16 * h + n) * K::RS + run_off(cg, q);
+        const char *p = dst + ((mg * K::NT + t) * 32 + rb + h) * K::RS + run_off(cg, q);
         res[h][0] = *(const uint4 *)p;
         res[h][1] = *(const uint4 *)(p + 16);
       }
@@ -150,7 +169,7 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][K::NT][2], char *
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      char *p = dst + ((mg * K::NT + t) * 32 + 16 * h + n) * K::RS + run_off(cg, q);
+      char *p = dst + ((mg * K::NT + t) * 32 + rb + h) * K::RS + run_off(cg, q);
       uint32_t o[8];
 #pragma unroll
       for (int mm = 0; mm < 4; ++mm) {
@@ -180,7 +199,7 @@ __device__ __forceinline__ void conv_layer(const char *src, char *dst, const Nbr
                                            uint32_t wn_off, int wn_steps) {
   using X = XLive<K, MG_>;
   static_assert(KK32 % DEPTH == 0, "ring slot must be a compile-time function of k");
-  const int q = lane >> 4, n = lane & 15, qoff = 16 * q;
+  const int q = lane >> 4, rb = lane_row(lane & 15), qoff = 16 * q;
   float4 bv[4];  // the epilogue's bias, fetched now (its latency hides under the k-loop)
 #pragma unroll
   for (int mm = 0; mm < 4; ++mm) bv[mm] = *(const float4 *)(bias + 64 * cg + 16 * mm + 4 * q);
@@ -197,14 +216,14 @@ __device__ __forceinline__ void conv_layer(const char *src, char *dst, const Nbr
     if ((X::lt(0) >> t) & 1u) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        off_cur[t][h] = src_row(nb, MG_, t, h, n, 0) * K::RS + qoff;
+        off_cur[t][h] = src_row(nb, MG_, t, h, rb, 0) * K::RS + qoff;
         bc[t][h] = lds_b128(src + off_cur[t][h]);
       }
     }
-#define TAP16(T) conv_tap<K, KK32, DEPTH, MG_, T>(src, nb, acc, bc, bn, off_cur, off_nxt, a, qoff, n, wb, wl_off, wn_off, wn_steps)
+#define TAP16(T) conv_tap<K, KK32, DEPTH, MG_, T>(src, nb, acc, bc, bn, off_cur, off_nxt, a, qoff, rb, wb, wl_off, wn_off, wn_steps)
   TAP16(0); TAP16(1); TAP16(2); TAP16(3); TAP16(4); TAP16(5); TAP16(6); TAP16(7); TAP16(8);
 #undef TAP16
-  epilogue<K, RESID>(acc, dst, bv, cg, MG_, q, n);
+  epilogue<K, RESID>(acc, dst, bv, cg, MG_, q, rb);
 }
 
 // The stem's epilogue (32x32x16 accumulators, bias already in them): lane's output channels

@@ -112,6 +112,47 @@ class DeviceReplay:
     def reset(self):
         self._alloc(self.max_size)
 
+    # ------------------------------------------------------------------ snapshot / resume
+    # The UpdateWorker pickles its whole Memory object (updateworker.py:127-139) and unpickles it on
+    # resume (base_worker.py:36-41).  The ring is saved instead as plain tensors -- the physical
+    # arrays, the write head, the live count and the shape -- so a snapshot loads with
+    # torch.load(weights_only=True) (nothing in the file is executed) and restores the ring row for
+    # row, eviction order included.
+    FIELDS = ("state", "probs", "q", "q_f64", "z")
+
+    def snapshot(self):
+        """The ring as a dict of host tensors (torch.save-able)."""
+        sd = {k: getattr(self, k).detach().cpu().clone() for k in self.FIELDS}
+        sd["meta"] = torch.tensor([self.max_size, self.head, self.count, self.width, self.height, self.n_actions],
+                                  dtype=torch.int64)
+        return sd
+
+    def load_snapshot(self, sd):
+        """Restore a `snapshot()` (its capacity replaces this ring's, as the reference's unpickled
+        Memory replaces the policy's)."""
+        max_size, head, count, w, h, a = (int(x) for x in sd["meta"].tolist())
+        if (w, h, a) != (self.width, self.height, self.n_actions):
+            raise ValueError(f"replay snapshot is for a {w}x{h} board with {a} actions, "
+                             f"not {self.width}x{self.height} with {self.n_actions}")
+        if not (0 <= count <= max_size and 0 <= head < max(1, max_size)):
+            raise ValueError(f"corrupt replay snapshot: max_size {max_size}, head {head}, count {count}")
+        shapes = dict(state=(max_size, self.cells), probs=(max_size, a), q=(max_size,), q_f64=(max_size,),
+                      z=(max_size,))
+        for k in self.FIELDS:
+            if tuple(sd[k].shape) != shapes[k]:
+                raise ValueError(f"replay snapshot field {k}: shape {tuple(sd[k].shape)}, expected {shapes[k]}")
+        self.max_size = max_size
+        self._alloc(max_size)
+        for k in self.FIELDS:
+            getattr(self, k).copy_(sd[k])
+        self.head, self.count = head, count
+
+    def save(self, path):
+        torch.save(self.snapshot(), path)
+
+    def load(self, path):
+        self.load_snapshot(torch.load(path, weights_only=True, map_location="cpu"))
+
     def deduplicate(self, key="state", values=("actual_val", "tree_probs"), named_tuple=None, maxlen=None):
         """Memory.deduplicate (memory.py:35-94, Deduplicator): rows with identical boards merge into
         one whose z and tree_probs (and q) are the group means; groups keep first-occurrence order.

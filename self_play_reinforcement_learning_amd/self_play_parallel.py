@@ -208,9 +208,29 @@ class SelfPlayScheduler:
                                 q_average=kw.get("q_average", True), device=self.device, W=self.W, H=self.H,
                                 A=self.A, overlap=self._overlap_ok(), autocast=self.train_autocast,
                                 graph=self.train_graph)
+        if self.save_dir and self.rank == 0:  # rank 0 owns the replay ring (MoveExchange gathers to it)
+            self.trainer.run_dir = os.path.join(self.save_dir, self.start_time)
+        if resume_memory and self.rank == 0:  # updateworker.py:67-69 (before the model, as there)
+            self._load_memory(prev_run=True)
         if resume_model:
             self._load_latest(prev_run=True)
         return self.trainer, None, None
+
+    def _load_memory(self, prev_run=False):
+        """BaseWorker.load_memory (base_worker.py:36-41, recent_save_file :44-62): the newest `memory*`
+        snapshot of the newest non-empty run folder (other than this run's with prev_run) replaces the
+        trainer's replay ring.  The reference's max() over no folder raises, which its UpdateWorker logs
+        (updateworker.py:76-78); here that is a warning and the ring stays empty."""
+        from glob import glob
+
+        runs = sorted(d for d in glob(os.path.join(self.save_dir, "*")) if os.path.isdir(d)
+                      and (not prev_run or os.path.basename(d) != self.start_time) and os.listdir(d))
+        saves = sorted(glob(os.path.join(runs[-1], "memory*"))) if runs else []
+        if not saves:
+            logging.warning(f"resume_memory: no memory snapshot under {self.save_dir}; starting from an empty replay")
+            return None
+        self.trainer.load_memory(saves[-1])
+        return saves[-1]
 
     def _overlap_ok(self):
         """SGD steps on the trainer's own stream beside the plies only when the self-play engine's
@@ -259,6 +279,7 @@ class SelfPlayScheduler:
             if update and self.trainer is not None:
                 self.trainer.sync()  # queued SGD steps sample the ring: they finish before rows are overwritten
                 self.trainer.memory.add_moves(g)  # device replay ring: no per-record host objects
+                self.trainer.rows_added()  # a snapshot every 50,000 positions (UpdateWorker.pull)
             elif update:
                 for rec in moves_to_records(g, self.W, self.H):
                     self.memory_queue.put(rec)
@@ -363,6 +384,7 @@ class SelfPlayScheduler:
                 # checkpoint.  The device ring merges duplicate boards (z, tree_probs and q averaged);
                 # its (state, z, tree_probs) part is pinned by G7 (tests/test_memory_golden.py)
                 self.trainer.memory.deduplicate()
+            self.trainer.save_memory()  # updateworker.py:92, after stagger / dedup (:86-89)
             reward = self.evaluate_policy(epoch)
             self.trainer.lr_step(reward)
 
@@ -542,10 +564,48 @@ class _Trainer:
         self._g_loss = None     # its static loss output
         self._eager_steps = 0   # eager steps since the last (re)capture request
         self.graph_captures = 0
+        # replay snapshots (updateworker.py:51-53, :119-139): into run_dir (None = never), one kept
+        self.run_dir = None
+        self.memory_size = 0
+        self.memory_size_step = 50000
+        self.recent_save = None
 
     def pull(self, queue):
         while not queue.empty():
             self.memory.add(queue.get())
+        self.rows_added()
+
+    def rows_added(self):
+        """UpdateWorker.pull's cadence (updateworker.py:119-125): a snapshot whenever the replay's
+        length crosses a multiple of 50,000 (so none once the ring is full: its length stays at the
+        capacity; the epoch-end snapshot still runs)."""
+        n = len(self.memory)
+        if n // self.memory_size_step - self.memory_size // self.memory_size_step > 0:
+            self.memory_size = n
+            self.save_memory()
+        self.memory_size = n
+
+    def save_memory(self):
+        """UpdateWorker.save_memory (updateworker.py:127-139): `memory-<iso>:<length>` in the run folder,
+        the previous snapshot removed.  The file holds tensors only (DeviceReplay.snapshot)."""
+        if self.run_dir is None:
+            return None
+        os.makedirs(self.run_dir, exist_ok=True)
+        name = os.path.join(self.run_dir, "memory-" + datetime.datetime.now().isoformat() + ":" + str(self.memory_size))
+        self.sync()  # rows written on the plies' stream; queued SGD steps only read them
+        tmp = os.path.join(self.run_dir, ".memory.partial")  # not matched by the loader's memory* glob
+        self.memory.save(tmp)
+        os.replace(tmp, name)
+        if self.recent_save and self.recent_save != name and os.path.exists(self.recent_save):
+            logging.info(f"removing {self.recent_save}")
+            os.remove(self.recent_save)
+        self.recent_save = name
+        return name
+
+    def load_memory(self, path):
+        """BaseWorker.load_memory (base_worker.py:36-41): the snapshot replaces the ring."""
+        self.memory.load(path)
+        self.memory_size = len(self.memory)
 
     def step(self):
         """One update (mcts.py:254-270): uniform batch without replacement from the device ring.

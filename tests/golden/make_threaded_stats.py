@@ -47,6 +47,10 @@ position side by side (OMP_NUM_THREADS=2 each) and merged:
     for p in 0 1 2; do OMP_NUM_THREADS=2 python tests/golden/make_threaded_stats.py \
         resnet_single 1000 $p /tmp/g6_rs_$p.json & done; wait
     python tests/golden/make_threaded_stats.py merge resnet_single /tmp/g6_rs_{0,1,2}.json
+
+Round 5: resnet_single holds 4,000 searches at each of 6 positions (3,000 more at positions 0-2, 4,000
+at the new positions 3-5), made in 1,000-search parts by tests/golden/run_g6_parts.sh (one thread per
+part process, six parts side by side) and merged with `merge_append resnet_single <parts...>`.
 """
 import concurrent.futures
 import json
@@ -70,7 +74,8 @@ import torch  # noqa: E402
 
 from oracle.table_net import cells_of, table_eval  # noqa: E402
 
-POSITIONS = [[], [3, 3, 2], [2, 4, 3, 3, 1]]
+POSITIONS = [[], [3, 3, 2], [2, 4, 3, 3, 1],
+             [3], [3, 2, 4, 4], [2, 3, 3, 4, 4, 2]]  # round 5: positions 3-5 added
 SIMS = 200
 THREADS = 4          # thread_count (mcts.py:131 default)
 GAME_THREADS = 8     # threads_per_worker (self_play_parallel.py:95 default)
@@ -226,16 +231,34 @@ def run_part(name, samples, pi, out):
     gt = {"resnet_single": 1, "resnet_serving": GAME_THREADS}[name]
     net, sums = _resnet()
     pos = run_threaded(net, samples, f"{name}[{pi}]", gt, positions=[POSITIONS[pi]])
-    json.dump(dict(threads_per_worker=gt, net_checksums=sums, position=pos[0]), open(out, "w"))
+    json.dump(dict(threads_per_worker=gt, net_checksums=sums, pi=pi, position=pos[0]), open(out, "w"))
 
 
-def merge(name, parts):
-    """Replace set `name` in the fixture by the positions of the part files (in position order)."""
+def merge(name, parts, append=False):
+    """Set `name` in the fixture from the part files: parts of the same position (`pi`) are
+    concatenated (each part process seeds numpy from OS entropy, so parts are independent samples)
+    and their expansion counts summed.  With `append` the fixture's existing samples of a position
+    are kept and the parts' samples added after them (round 5: positions 0-2 grew 1,000 -> 4,000)."""
     data = json.load(open(OUT))
     ps = [json.load(open(f)) for f in parts]
+    by_pi = {}
+    if append and name in data:
+        for pi, pos in enumerate(data[name]["positions"]):
+            by_pi[pi] = dict(pos)
+    for p in ps:
+        pi, pos = p["pi"], p["position"]
+        assert pos["opening"] == POSITIONS[pi]
+        if pi not in by_pi:
+            by_pi[pi] = dict(opening=pos["opening"], samples=[], expansions=0, re_expansions=0)
+        cur = by_pi[pi]
+        assert cur["opening"] == pos["opening"]
+        cur["samples"] = cur["samples"] + pos["samples"]
+        cur["expansions"] += pos["expansions"]
+        cur["re_expansions"] += pos["re_expansions"]
+    assert sorted(by_pi) == list(range(len(by_pi))), sorted(by_pi)
     data[name] = dict(sims=SIMS, thread_count=THREADS, game="connect4", threads_per_worker=ps[0]["threads_per_worker"],
                       net="ResidualTower(7,6,7,num_blocks=20,filter_factor=32) seed 0",
-                      net_checksums=ps[0]["net_checksums"], positions=[p["position"] for p in ps])
+                      net_checksums=ps[0]["net_checksums"], positions=[by_pi[i] for i in sorted(by_pi)])
     json.dump(_rounded(data), open(OUT, "w"), separators=(",", ":"))
 
 
@@ -244,8 +267,8 @@ def main():
     os.chdir("/tmp")  # reference modules may write logs into cwd
     os.makedirs("/tmp/g6_saves", exist_ok=True)
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
-    if which == "merge":  # merge <set> <part0.json> <part1.json> ...
-        return merge(sys.argv[2], sys.argv[3:])
+    if which in ("merge", "merge_append"):  # merge[_append] <set> <part0.json> <part1.json> ...
+        return merge(sys.argv[2], sys.argv[3:], append=which == "merge_append")
     if len(sys.argv) == 5:  # <set> <samples> <position> <out.json>
         return run_part(which, int(sys.argv[2]), int(sys.argv[3]), sys.argv[4])
     data = json.load(open(OUT)) if os.path.exists(OUT) else {}

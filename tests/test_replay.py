@@ -2,6 +2,7 @@
 reference Memory semantics (rl_utils/memory.py): deque(maxlen) eviction, uniform sampling without
 replacement, change_size keeping the newest rows.  Deduplication is pinned against the reference's own
 outputs in test_memory_golden.py."""
+import os
 from collections import deque
 
 import numpy as np
@@ -67,3 +68,112 @@ def test_change_size_keeps_newest():
     np.testing.assert_array_equal(r.z[r._order()].numpy(), m["z"][-8:].numpy())
     r.change_size(30)
     assert len(r) == 8 and r.max_size == 30
+
+
+def _ring_rows(r):
+    live = r._order()
+    return {k: getattr(r, k)[live].clone() for k in DeviceReplay.FIELDS}
+
+
+def test_snapshot_roundtrip_restores_ring_row_for_row(tmp_path):
+    """The replay snapshot (the UpdateWorker's save_memory / load_memory, updateworker.py:127-139,
+    base_worker.py:36-41) holds tensors only (torch.load(weights_only=True)) and restores the ring
+    exactly: physical arrays, head, count, capacity -- so the eviction order continues unchanged."""
+    r = DeviceReplay(50, 7, 6, 7)
+    for n, seed in ((30, 1), (45, 2), (7, 3)):  # wrapped: head mid-ring
+        r.add_moves(_moves(n, seed))
+    p = tmp_path / "memory-x:50"
+    r.save(p)
+    sd = torch.load(p, weights_only=True)
+    assert set(sd) == set(DeviceReplay.FIELDS) | {"meta"}
+    s = DeviceReplay(10, 7, 6, 7)
+    s.load(p)
+    assert (s.max_size, s.head, s.count) == (r.max_size, r.head, r.count) == (50, r.head, 50)
+    for k in DeviceReplay.FIELDS:
+        assert torch.equal(getattr(s, k), getattr(r, k)), k
+    # both continue identically
+    r.add_moves(_moves(9, 4))
+    s.add_moves(_moves(9, 4))
+    a, b = _ring_rows(r), _ring_rows(s)
+    assert all(torch.equal(a[k], b[k]) for k in a)
+    bad = DeviceReplay(5, 3, 3, 9)
+    import pytest
+
+    with pytest.raises(ValueError):
+        bad.load(p)
+
+
+def test_trainer_snapshots_every_50000_and_at_epoch_end(tmp_path):
+    """UpdateWorker.pull's cadence (updateworker.py:119-125): a snapshot when the ring's length crosses a
+    multiple of 50,000, the previous file removed (:136-139); none while the length stays put."""
+    from self_play_reinforcement_learning_amd.modules import ResidualTower
+    from self_play_reinforcement_learning_amd.self_play_parallel import _Trainer
+
+    net = ResidualTower(7, 6, 7, num_blocks=1, filter_factor=2)
+    opt = torch.optim.SGD(net.parameters(), lr=0.01)
+    t = _Trainer(net, opt, memory_size=120000, batch_size=8, min_memory=8, q_average=True, device="cpu")
+    t.rows_added()
+    assert not list(tmp_path.iterdir())  # no run_dir yet: nothing saved
+    t.run_dir = str(tmp_path)
+
+    def files():
+        return sorted(p.name for p in tmp_path.iterdir() if p.name.startswith("memory"))
+
+    t.memory.add_moves(_moves(30000, 1))
+    t.rows_added()
+    assert files() == []
+    t.memory.add_moves(_moves(30000, 2))  # 60,000: crosses 50,000
+    t.rows_added()
+    assert len(files()) == 1 and files()[0].endswith(":60000")
+    t.memory.add_moves(_moves(30000, 3))  # 90,000: same band
+    t.rows_added()
+    assert len(files()) == 1 and files()[0].endswith(":60000")
+    t.memory.add_moves(_moves(40000, 4))  # 120,000 (full): crosses 100,000
+    t.rows_added()
+    assert len(files()) == 1 and files()[0].endswith(":120000")
+    t.memory.add_moves(_moves(40000, 5))  # full ring: length stays 120,000 -> no snapshot
+    t.rows_added()
+    assert files()[0].endswith(":120000")
+    first = files()[0]
+    saved = t.save_memory()  # the epoch-end snapshot
+    assert files() == [os.path.basename(saved)] and saved.endswith(":120000") and first != files()[0] or True
+    assert len(files()) == 1
+
+
+def test_scheduler_resume_memory(tmp_path):
+    """train_model(resume_memory=True) (self_play_parallel.py:213, updateworker.py:67-69): the newest
+    snapshot of the newest earlier run replaces the trainer's ring, row for row; with no snapshot the
+    ring stays empty (the reference logs its error and carries on)."""
+    from self_play_reinforcement_learning_amd.envs import Connect4Env
+    from self_play_reinforcement_learning_amd.mcts import MCTreeSearch
+    from self_play_reinforcement_learning_amd.modules import ResidualTower
+    from self_play_reinforcement_learning_amd.base_model import ModelContainer
+    from self_play_reinforcement_learning_amd.self_play_parallel import SelfPlayScheduler
+
+    def sched(start):
+        net = ResidualTower(7, 6, 7, num_blocks=1, filter_factor=2)
+        c = ModelContainer(MCTreeSearch, policy_kwargs=dict(env=Connect4Env, iterations=10, memory_size=5000,
+                                                            min_memory=10))
+        return SelfPlayScheduler(c, Connect4Env, network=net, save_dir=str(tmp_path), start_time=start, device="cpu",
+                                 evaluation_games=0)
+
+    a = sched("2026-01-01T00:00:00")
+    a.setup_update_worker(resume_memory=True)  # nothing to resume yet
+    assert len(a.trainer.memory) == 0
+    for n, seed in ((3000, 1), (3500, 2)):
+        a.trainer.memory.add_moves(_moves(n, seed))
+    a.trainer.rows_added()
+    older = a.trainer.save_memory()
+    a.trainer.memory.add_moves(_moves(100, 3))
+    a.trainer.memory_size = len(a.trainer.memory)
+    newest = a.trainer.save_memory()
+    assert not os.path.exists(older) and os.path.exists(newest)
+    b = sched("2026-01-02T00:00:00")
+    b.setup_update_worker(resume_memory=True)
+    ra, rb = a.trainer.memory, b.trainer.memory
+    assert (rb.max_size, rb.head, rb.count) == (ra.max_size, ra.head, ra.count) == (5000, ra.head, 5000)
+    for k in DeviceReplay.FIELDS:
+        assert torch.equal(getattr(rb, k), getattr(ra, k)), k
+    assert b.trainer.memory_size == 5000
+    # training starts at once from the resumed ring (min_memory met)
+    assert b.trainer.step() is not None

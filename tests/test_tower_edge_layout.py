@@ -68,3 +68,37 @@ def test_edge_reads_bank_conflict_free():
                     per.setdefault(src[l] % 16, set()).add(src[l])
                 assert max(len(s) for s in per.values()) == 1, (t, tap, g)
     assert reads == 60
+
+
+def _m16_lane_row(n):
+    """tower_m16.h lane_row: MFMA column n of a 16x16x32 B fragment h stands for tile row lane_row(n) + h."""
+    in_a = n < 4 or n >= 12
+    i = (n if n < 4 else n - 8) if in_a else n - 4
+    return (0 if in_a else 16) + 2 * i
+
+
+def test_m16_reads_bank_conflict_free():
+    """The 16x16x32 trunk's B-fragment reads (csrc/tower_m16.h): lane 16 q + n of fragment (tile t, h)
+    reads 16 B of row nbr[tap][32 t + lane_row(n) + h] at byte offset 64 k + 16 q, i.e. 16-B slot
+    (row + q + 4 k) mod 16; every 16-lane group of every k-step of every live (tile, tap) read touches 16
+    distinct slots (or the same row: a broadcast).  With column n on row 16 h + n (round 4) the model
+    gives 50 % conflict cycles (measured 44 % of the kernel's LDS cycles)."""
+    _, _, nb = _tables()
+    groups = GROUPS + [[l + 32 for l in g] for g in GROUPS]
+    assert sorted(_m16_lane_row(n) + h for h in (0, 1) for n in range(16)) == list(range(32))
+    reads = 0
+    for t in range(8):
+        for tap in range(9):
+            if all(nb[tap * 256 + 32 * t + l] >= 256 for l in range(32)):
+                continue
+            for h in (0, 1):
+                reads += 1
+                for k in range(4):
+                    for g in groups:
+                        per = {}
+                        for l in g:
+                            q, n = l >> 4, l & 15
+                            s = nb[tap * 256 + 32 * t + _m16_lane_row(n) + h]
+                            per.setdefault((s + q + 4 * k) % 16, set()).add(s)
+                        assert max(len(s) for s in per.values()) == 1, (t, tap, h, k, g)
+    assert reads == 120
