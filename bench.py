@@ -254,9 +254,9 @@ def main():
                          "default) is the reference's own inference dtype (amp.autocast, inference_worker.py:117)")
     ap.add_argument("--secondary", action="store_true",
                     help="also time the other trunk dtype (bf16 <-> fp16) on a fresh engine with the same seeds, "
-                         "--warmup and --steps, reported as secondary_dtype.  Off by default: bf16's search shift is "
-                         "pinned only at 0.03 (tests/test_gpu_statistical.py SHIFT_TOL), a bound that does not reject "
-                         "a serial search, so the headline runs fp16 alone")
+                         "--warmup and --steps, reported as secondary_dtype.  Off by default: the headline runs the "
+                         "reference's inference dtype (fp16) alone; bf16's search shift is bounded at 0.02 "
+                         "(tests/test_gpu_statistical.py SHIFT_TOL), eight times fp16's error")
     ap.add_argument("--no-secondary", dest="secondary", action="store_false", help=argparse.SUPPRESS)
     ap.add_argument("--search-threads", type=int, default=4,
                     help="sims in flight per tree with virtual loss: the reference's thread_count search "

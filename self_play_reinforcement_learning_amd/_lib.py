@@ -164,6 +164,22 @@ def lib():
     return _lib
 
 
+# environment switches read only by the A/B library (libspmcts_ab.so); the product library refuses them with
+# SPMCTS_ERR_AB_SWITCH (-5, include/spmcts.h) rather than silently ignoring them
+AB_SWITCHES = ("SPMCTS_TOWER_CG", "SPMCTS_TOWER_RING", "SPMCTS_TOWER_C256", "SPMCTS_WIDE_TAILS", "SPMCTS_HEADS",
+               "SPMCTS_HEADS_C256", "SPMCTS_TREE_BLOCK", "SPMCTS_EXPAND_CO", "SPMCTS_TOWER_M16")
+ERR_AB_SWITCH = -5
+
+
+def tower_error(what, rc):
+    """The SpmctsError of a failed tower entry point; -5 names the A/B switch that caused it."""
+    if rc == ERR_AB_SWITCH:
+        set_ = [n for n in AB_SWITCHES if n in os.environ]
+        return SpmctsError(f"{what} failed ({rc}): {', '.join(set_) or 'an A/B switch'} is set, a switch of the A/B "
+                           f"library (make ab: libspmcts_ab.so, SPMCTS_LIB=...); unset it to use the product library")
+    return SpmctsError(f"{what} failed ({rc})")
+
+
 def check(rc, what=""):
     if rc != 0:
         msg = lib().spmcts_last_error().decode(errors="replace")

@@ -536,7 +536,16 @@ class LanedEngine:
         else:
             self.select_timer = self.expand_timer = self.nn_timer = self.tower_timer = None
 
-    def refresh_network(self):
+    def refresh_network(self, on_moves=None):
+        """New weights for every lane.  A staggered lane may hold a half-finished ply (between ply()
+        calls): it is finished on the old weights first (drain, its Moves to `on_moves`), so no search
+        mixes evaluations of two weight versions; without `on_moves` that would drop its finished games'
+        Moves, so it raises instead (run() and play_games() return drained)."""
+        if getattr(self, "_pending", False):
+            if on_moves is None:
+                raise RuntimeError("refresh_network with a staggered ply in flight: pass on_moves (or call "
+                                   "drain(on_moves) first) so the games it finishes are not dropped")
+            self.drain(on_moves)
         self._lanes_wait_caller()
         self._each(lambda e: e.refresh_network())
 

@@ -403,7 +403,7 @@ class HipTowerEvaluator(Evaluator):
         if timer is not None:
             timer.stop()
         if rc != 0:
-            raise self._lib.SpmctsError(f"spmcts_tower_forward_dev failed ({rc})")
+            raise self._lib.tower_error("spmcts_tower_forward_dev", rc)
 
     def heads_dev(self, count_dev, max_rows):
         """The linear-heads half of forward_dev (k_heads) on the current stream."""
@@ -415,7 +415,7 @@ class HipTowerEvaluator(Evaluator):
                                                     c(self.head_b.data_ptr()), c(probs.data_ptr()),
                                                     c(values.data_ptr()), self.flags, stream)
         if rc != 0:
-            raise self._lib.SpmctsError(f"spmcts_tower_heads_dev failed ({rc})")
+            raise self._lib.tower_error("spmcts_tower_heads_dev", rc)
         return probs, values
 
     @torch.no_grad()
@@ -430,7 +430,7 @@ class HipTowerEvaluator(Evaluator):
                 self._lib.ctypes.c_void_p(self.wblob.data_ptr()), self._lib.ctypes.c_void_p(self.bblob.data_ptr()),
                 self._lib.ctypes.c_void_p(feats.data_ptr()), self.flags, self._lib.ctypes.c_void_p(stream))
             if rc != 0:
-                raise self._lib.SpmctsError(f"spmcts_tower_forward failed ({rc})")
+                raise self._lib.tower_error("spmcts_tower_forward", rc)
         return feats[:n]
 
     @torch.no_grad()
@@ -451,7 +451,7 @@ class HipTowerEvaluator(Evaluator):
                     self.hid, self.A, c(z.data_ptr()), z.shape[1], n, c(self.epi_b.data_ptr()), c(probs.data_ptr()),
                     c(value.data_ptr()), c(torch.cuda.current_stream().cuda_stream))
                 if rc != 0:
-                    raise self._lib.SpmctsError(f"spmcts_head_epilogue failed ({rc})")
+                    raise self._lib.tower_error("spmcts_head_epilogue", rc)
             return probs[:n], value[:n]
         if self.fused_heads:
             probs = torch.empty((max(n, 1), self.A), dtype=torch.float32, device=f.device)
@@ -463,7 +463,7 @@ class HipTowerEvaluator(Evaluator):
                     c(self.head_b.data_ptr()), c(probs.data_ptr()), c(value.data_ptr()), self.flags,
                     c(torch.cuda.current_stream().cuda_stream))
                 if rc != 0:
-                    raise self._lib.SpmctsError(f"spmcts_tower_heads failed ({rc})")
+                    raise self._lib.tower_error("spmcts_tower_heads", rc)
             return probs[:n], value[:n]
         pf = f[:, :, : self.ff].reshape(n, -1)
         vf = f[:, :, self.ff:].reshape(n, -1)

@@ -662,7 +662,7 @@ class _Trainer:
             dst.copy_(src)
         self._g.replay()
         self.network.eval()  # the captured step ran in train mode; module flags are host state
-        return self._g_loss.detach()
+        return self._g_loss.detach().clone()  # the static output is overwritten by the next replay
 
     def _capture(self, s, z, pi, q):
         self._g_in = tuple(t.detach().clone() for t in (s, z, pi, q))

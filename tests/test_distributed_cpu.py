@@ -314,6 +314,24 @@ def test_staggered_play_games_single_process():
     assert per1 == ["begin", 0, 1, 2, 3, "move", "finish"] * eng.lanes[1].plies_run
 
 
+def test_staggered_refresh_network_finishes_the_ply_in_flight():
+    """LanedEngine.refresh_network with a staggered ply in flight: without a Move sink it refuses (the
+    drained ply's finished games would be dropped); with one it completes the ply on the old weights first,
+    then refreshes every lane -- no search mixes two weight versions."""
+    log = []
+    eng = _staggered_engine(log)
+    for ln in eng.lanes:
+        ln.refresh_network = (lambda ln=ln: log.append((ln.idx, "refresh")))
+    eng.ply()
+    assert eng._pending
+    with pytest.raises(RuntimeError):
+        eng.refresh_network()
+    eng.refresh_network(on_moves=lambda m: None)
+    assert not eng._pending
+    assert log[-2:] == [(0, "refresh"), (1, "refresh")]
+    assert log.index((1, "finish"), log.index((0, "finish")) + 1) < log.index((0, "refresh"))
+
+
 def test_pack_unpack_roundtrip():
     m = _moves(0, 9)
     back = D.unpack_moves(D.pack_moves(m), 42, 7)
