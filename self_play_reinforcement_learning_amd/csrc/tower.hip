@@ -1583,7 +1583,7 @@ static bool c256_board3() {  // SPMCTS_TOWER_C256=3: the C = 256 trunk on 3-boar
   static const bool v = env_is("SPMCTS_TOWER_C256", "3");
   return v;
 }
-static bool wide_tails3() {  // SPMCTS_WIDE_TAILS=3: packed C = 256 launches with 3-board tail code
+static bool wide_tails3() {  // SPMCTS_WIDE_TAILS=3: C = 256 launches with 3-board tail code
   static const bool v = env_is("SPMCTS_WIDE_TAILS", "3");
   return v;
 }
@@ -1651,14 +1651,15 @@ static int forward_dev(int32_t width, int32_t height, int32_t channels, int32_t 
 #ifdef SPMCTS_AB
     if (c256_board3())
       return launch_dyn<K3, K3, K3>(planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, pack, s);
-    if (pack && !wide_tails3())
-#else
-    // packed launches (lanes beside each other) have a tail of < 6 boards: one 6-board tile takes it, and a
-    // kernel with the one-buffer code path only holds fewer registers
-    if (pack)
+    if (wide_tails3())  // SPMCTS_WIDE_TAILS=3: the round-3 set, 3-board tail tiles in one kernel with the 6-board body
+      return launch_dyn<KW, K3, K3>(planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, pack,
+                                    s);
 #endif
-      return launch_dyn<KW, KW, KW>(planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, pack, s);
-    return launch_dyn<KW, K3, K3>(planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, pack, s);
+    // every tile a 6-board one-buffer tile (a batch tail takes one partly empty tile): a kernel that holds the
+    // one-buffer code path only (the set with 3-board tail code inlined beside it spilled twice as much; the
+    // outputs are the same bits either way, test_wide_c256_tiles_bit_identical)
+    (void)sizeof(K3);
+    return launch_dyn<KW, KW, KW>(planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, pack, s);
   }
   if (width == 3 && height == 3 && channels == 128)
     return launch_dyn<Cfg<128, 256, 3, 3, 2, 4, 0, 4, 1, false, false, E>, Cfg<128, 192, 3, 3, 2, 4, 0, 4, 1, false, false, E>,

@@ -164,12 +164,14 @@ __device__ __forceinline__ void conv(char *X, const Nbr<K> &nb, bf16x8 (&a)[DEPT
       if ((ZP >> t) & 1u) acc[m][t] = f32x16{};
   int off_cur[K::NT], off_nxt[K::NT];
   bf16x8 bc[K::NT], bn[K::NT];
+  // tap 0's operand rows from the LDS table at each layer start (one round trip per layer) rather than
+  // 8 offsets held in registers through every layer: at 512 registers they were spilled and reloaded
 #pragma unroll
   for (int t = 0; t < K::NT; ++t)
-    if ((LV0 >> t) & 1u) {
-      off_cur[t] = nb.off0[t] + hoff;
-      bc[t] = lds_b128(X + off_cur[t]);
-    }
+    if ((LV0 >> t) & 1u) off_cur[t] = nb.off(t, 0) + hoff;
+#pragma unroll
+  for (int t = 0; t < K::NT; ++t)
+    if ((LV0 >> t) & 1u) bc[t] = lds_b128(X + off_cur[t]);
 #define TAPW(T) conv_tap_x<K, KK, DEPTH, 0, T>(X, nb, acc, bc, bn, off_cur, off_nxt, a, hoff, wb, wl_off, wn_off, wn_steps)
   TAPW(0); TAPW(1); TAPW(2); TAPW(3); TAPW(4); TAPW(5); TAPW(6); TAPW(7); TAPW(8);
 #undef TAPW
@@ -271,14 +273,17 @@ __device__ __forceinline__ void tile(char *smem, const __bf16 *planes, int batch
   wb.voff = lane * 16;
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   const uint32_t ct0_off = (uint32_t)(STEM + (size_t)(wave_u * K::MT) * LSTEPS * 64) * 16u;
-  for (int L = 0; L < n_convs; ++L) {
+  // one loop iteration per residual block: its first conv, then its second (residual + save) -- a straight
+  // line, where an odd/even branch per conv made the register allocator merge the two bodies' live ranges
+  // at the branch (66 spilled VGPRs in round 4, reloaded there)
+  for (int L = 0; L < n_convs; L += 2) {
     const uint32_t wl_off = ct0_off + (uint32_t)((size_t)L * LAYER * 16u);
-    const uint32_t wn_off = (kRingAlways && L + 1 == n_convs) ? wl_off : wl_off + (uint32_t)(LAYER * 16u);
-    const int wn_steps = L + 1 < n_convs ? LSTEPS : 0;
-    if ((L & 1) == 0)
-      conv<K, KK, DEPTH, false, false>(X, nb, ring, b, wave, lane, wb, wl_off, wn_off, wn_steps, scr, sbias);
-    else
-      conv<K, KK, DEPTH, true, true>(X, nb, ring, b, wave, lane, wb, wl_off, wn_off, wn_steps, scr, sbias);
+    conv<K, KK, DEPTH, false, false>(X, nb, ring, b, wave, lane, wb, wl_off, wl_off + (uint32_t)(LAYER * 16u), LSTEPS,
+                                     scr, sbias);
+    b += K::C;
+    const uint32_t wl1 = wl_off + (uint32_t)(LAYER * 16u);
+    const uint32_t wn1 = (kRingAlways && L + 2 == n_convs) ? wl1 : wl1 + (uint32_t)(LAYER * 16u);
+    conv<K, KK, DEPTH, true, true>(X, nb, ring, b, wave, lane, wb, wl1, wn1, L + 2 < n_convs ? LSTEPS : 0, scr, sbias);
     b += K::C;
   }
   head_layer<K>(X, wblk + (size_t)n_convs * LAYER, b, out, board0, batch, wave, lane);
