@@ -2,7 +2,7 @@
 # rows read from the LDS table per layer (spills 66 -> 20), and every device-count tile a 6-board tile, against
 # round 4's library (ab_libs/libspmcts_r04.so), one box: (1) bit-equality of the outputs (ResNet-256, 2 and 20
 # blocks, host and device-count paths, fp16 and bf16); (2) the C = 256 tile test (6-board vs 3-board tiles);
-# (3) config 3 (16,384 games, 800 sims, ResNet-256x20), plies 3-6, alternated.
+# (3) config 3 (16,384 games, 800 sims, ResNet-256x20), plies 3-6, alternated; (4) the config-5 arena test.
 set -u
 O=gpurun_out/r05b
 mkdir -p $O
@@ -26,4 +26,6 @@ for rep in 1 2; do
     echo "config3 plies 3-6 $v: $(python3 -c "import json; d=json.loads([l for l in open('$O/c3_${v}_$rep.json') if l.startswith('{')][0]); print(round(d['value'],1), round(d['roofline']['frac'],4), round(d['roofline']['avg_launch_us'],1))")" | tee -a $O/summary.txt
   done
 done
+timeout -k 10 400 python -u -m pytest tests/test_gpu_engine.py -m gpu -x -v -s --timeout 360 --timeout-method thread -k "config5" > $O/config5_test.log 2>&1
+rc=$?; grep -E "config5:|passed|failed" $O/config5_test.log | tee -a $O/summary.txt; [ $rc -eq 0 ] || { tail -40 $O/config5_test.log; exit $rc; }
 exit 0
