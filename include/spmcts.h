@@ -312,6 +312,25 @@ int spmcts_tower_heads_dev(int32_t width, int32_t height, int32_t channels, int3
                            const int32_t *count_dev, int32_t max_batch, const void *head_w_dev,
                            const float *head_b_dev, float *probs_dev, float *values_dev, int32_t flags,
                            spmcts_stream stream);
+/* The trainer's 3x3 residual-block convolutions (stride 1, padding 1) on the matrix cores, fp16 NCHW tensors
+ * as torch autocast hands them to conv2d (replaces MIOpen's conv2d forward / backward-data / backward-weight
+ * calls that the UpdateWorker's autocast SGD step makes, updateworker.py:141-149 -> mcts.py:254-270 ->
+ * modules.py:13-40); fp32 accumulation, deterministic (no atomics).
+ *   _supported: 1 if the (board, channels) shape is handled, in both directions (forward and input grad).
+ *   _pack: w [cout][cin][3][3] -> wf [cout][9][cin] (forward) and wb [cin][9][cout] (taps flipped: the
+ *          input-gradient convolution's weights).
+ *   _fwd: y [n][cout][W][H] = bias + conv(x [n][cin][W][H], wpk = wf of _pack); bias may be NULL.  The input
+ *         gradient is _fwd(dy, wb) with cin and cout swapped and no bias.
+ *   _wgrad: dw [cout][cin][3][3] (fp16) = sum over the batch of dy x x-patches, split over `splits` board
+ *           groups into part [splits][cout][9][cin] (f32 scratch) and summed in order; db [cout] (fp16, may
+ *           be NULL) = sum of dy over the batch and cells.
+ * Return 0, -1 bad argument, -2 unsupported shape, -3 launch error. */
+int spmcts_conv3x3_supported(int32_t width, int32_t height, int32_t cin, int32_t cout);
+int spmcts_conv3x3_pack(int32_t cin, int32_t cout, const void *w, void *wf, void *wb, spmcts_stream stream);
+int spmcts_conv3x3_fwd(int32_t n, int32_t width, int32_t height, int32_t cin, int32_t cout, const void *x,
+                       const void *wpk, const void *bias, void *y, spmcts_stream stream);
+int spmcts_conv3x3_wgrad(int32_t n, int32_t width, int32_t height, int32_t cin, int32_t cout, const void *x,
+                         const void *dy, float *part, int32_t splits, void *dw, void *db, spmcts_stream stream);
 /* Memory-roofline helper: device copy bandwidth probe (bytes each way). */
 int spmcts_copy_probe(const void *src_dev, void *dst_dev, uint64_t bytes, spmcts_stream stream);
 

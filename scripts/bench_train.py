@@ -20,7 +20,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def run(args, updates, overlap, autocast=True, graph=True):
+def run(args, updates, overlap, autocast=True, graph=True, hip_convs=True):
     import torch
 
     from self_play_reinforcement_learning_amd import Connect4Env, MCTreeSearch, ModelContainer, SelfPlayScheduler
@@ -31,7 +31,7 @@ def run(args, updates, overlap, autocast=True, graph=True):
     kw = dict(iterations=args.sims, env=Connect4Env, batch_size=64, memory_size=200000, min_memory=args.min_memory)
     sp = SelfPlayScheduler(ModelContainer(MCTreeSearch, policy_kwargs=kw), Connect4Env, network=net, save_dir=None,
                            n_games=args.games, updates_per_ply=updates, overlap_training=overlap, evaluation_games=0,
-                           train_autocast=autocast, train_graph=graph,
+                           train_autocast=autocast, train_graph=graph, train_hip_convs=hip_convs,
                            lr=0.001)
     sp.setup_player_workers()
     sp.setup_update_worker()
@@ -58,15 +58,17 @@ def run(args, updates, overlap, autocast=True, graph=True):
     moves, steps = eng.counters()["moves"] - m0, tr.steps - s0
     loss = float(tr.last_loss) if tr.last_loss is not None else None
     return dict(updates_per_ply=updates, trainer_stream=tr.stream is not None, train_autocast=autocast, train_graph=graph,
+                train_hip_convs=tr.hip_convs,
                 graph_captures=tr.graph_captures, plies=args.plies, seconds=dt,
                 positions_per_s=moves / dt, sgd_steps=steps, sgd_steps_per_s=steps / dt, fill_plies=fill_plies,
                 replay_rows=len(tr.memory), last_loss=loss)
 
 
-def trainer_only(args, graph, autocast=True, steps=40, channels_last=False, benchmark=False):
+def trainer_only(args, graph, autocast=True, steps=40, channels_last=False, benchmark=False, hip_convs=True):
     """ms per SGD step of the trainer alone (batch 64, ResNet-128x20, train mode), graphed or eager;
     `channels_last`: the network's tensors in NHWC order; `benchmark`: MIOpen's exhaustive kernel search
-    (torch.backends.cudnn.benchmark)."""
+    (torch.backends.cudnn.benchmark); `hip_convs`: the residual blocks' 3x3 convolutions on the HIP
+    matrix-core kernels (trainconv.py; under autocast only) instead of MIOpen."""
     import torch
 
     from self_play_reinforcement_learning_amd.modules import ResidualTower
@@ -79,7 +81,7 @@ def trainer_only(args, graph, autocast=True, steps=40, channels_last=False, benc
         net = net.to(memory_format=torch.channels_last)
     tr = _Trainer(net, torch.optim.SGD(net.parameters(), lr=0.001, momentum=0.9, weight_decay=1e-4), memory_size=200000,
                   batch_size=64, min_memory=0, q_average=True, device="cuda", overlap=True, autocast=autocast,
-                  graph=graph)
+                  graph=graph, hip_convs=hip_convs)
     g = torch.Generator().manual_seed(0)
     n = 20000
     tr.memory.add_moves(dict(state=torch.randint(-1, 2, (n, 42), dtype=torch.int8, generator=g),
@@ -96,7 +98,8 @@ def trainer_only(args, graph, autocast=True, steps=40, channels_last=False, benc
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     torch.backends.cudnn.benchmark = False
-    return dict(train_graph=graph, train_autocast=autocast, channels_last=channels_last, benchmark=benchmark, steps=steps,
+    return dict(train_graph=graph, train_autocast=autocast, train_hip_convs=tr.hip_convs, channels_last=channels_last,
+                benchmark=benchmark, steps=steps,
                 ms_per_sgd_step=dt / steps * 1e3, graph_captures=tr.graph_captures, last_loss=float(tr.last_loss))
 
 
@@ -112,20 +115,30 @@ def main():
                          "no self-play runs")
     ap.add_argument("--trainer-only-graph", action="store_true",
                     help="only the graphed fp16-autocast trainer-only timing (for a kernel trace)")
+    ap.add_argument("--miopen-convs", action="store_true", help="with --trainer-only-graph: MIOpen's block convs")
+    ap.add_argument("--conv-ab", action="store_true",
+                    help="graphed autocast trainer-only timings, HIP block convs vs MIOpen, alternated 3 times")
     args = ap.parse_args()
     if args.trainer_only_graph:
-        print(json.dumps(dict(trainer_only=[trainer_only(args, True, steps=100)])), flush=True)
+        print(json.dumps(dict(trainer_only=[trainer_only(args, True, steps=100, hip_convs=not args.miopen_convs)])),
+              flush=True)
+        return
+    if args.conv_ab:
+        rows = [trainer_only(args, True, steps=100, hip_convs=h) for _ in range(3) for h in (True, False)]
+        print(json.dumps(dict(trainer_only=rows)), flush=True)
         return
     if args.trainer_variants:
         rows = [trainer_only(args, True, autocast=a, channels_last=c, benchmark=b)
                 for a in (True, False) for c in (False, True) for b in (False, True)]
         print(json.dumps(dict(trainer_only=rows)), flush=True)
         return
-    out = dict(workload=f"connect4 self-play + training, {args.sims} sims, {args.games} games, ResNet-128x20 (bf16 "
-                        f"trunk for leaves, SGD batch 64 under fp16 autocast as updateworker.py:148, or fp32), K = 4, two lanes",
-               trainer_only=[trainer_only(args, True), trainer_only(args, False), trainer_only(args, True, False)],
-               runs=[run(args, args.updates, True), run(args, args.updates, True, graph=False),
-                     run(args, args.updates, False), run(args, 0, True)])
+    out = dict(workload=f"connect4 self-play + training, {args.sims} sims, {args.games} games, ResNet-128x20 (fp16 "
+                        f"fused trunk for leaves, the bench default; SGD batch 64 under fp16 autocast as "
+                        f"updateworker.py:148), K = 4, two lanes",
+               trainer_only=[trainer_only(args, True), trainer_only(args, True, hip_convs=False),
+                             trainer_only(args, False)],
+               runs=[run(args, args.updates, False), run(args, args.updates, False, hip_convs=False),
+                     run(args, args.updates, True), run(args, 0, False)])
     print(json.dumps(out), flush=True)
 
 

@@ -125,6 +125,10 @@ _SIGS = {
     "spmcts_set_leaf_dedup": [_P, _I32],
     "spmcts_leaf_trees": [_P, _P, _P],
     "spmcts_copy_probe": [_P, _P, _U64, _P],
+    "spmcts_conv3x3_supported": [_I32, _I32, _I32, _I32],
+    "spmcts_conv3x3_pack": [_I32, _I32, _P, _P, _P, _P],
+    "spmcts_conv3x3_fwd": [_I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P],
+    "spmcts_conv3x3_wgrad": [_I32, _I32, _I32, _I32, _I32, _P, _P, _P, _I32, _P, _P, _P],
     "spmcts_tower_forward": [_I32, _I32, _I32, _I32, _P, _I32, _P, _P, _P, _I32, _P],
     "spmcts_tower_supported": [_I32, _I32, _I32],
     "spmcts_tower_weight_layout": [_I32, _I32, _I32],

@@ -93,7 +93,8 @@ class SelfPlayScheduler:
                  save_dir="saves", epoch_length=500, initial_games=64, lr=0.001, stagger=False, evaluation_games=100,
                  evaluation_network=None, stagger_mem_step=5000, deduplicate=False, update_delay=0.01,
                  self_play=None, n_games=None, device=None, seed=0, updates_per_ply=4, lanes=None, exchange_every=8,
-                 gpus=None, start_time=None, overlap_training=False, train_autocast=True, train_graph=True):
+                 gpus=None, start_time=None, overlap_training=False, train_autocast=True, train_graph=True,
+                 train_hip_convs=True):
         # constructor arguments, for rank processes started by this scheduler (_run_ranks)
         self._init_kwargs = {k: v for k, v in locals().items() if k not in ("self", "__class__")}
         self.policy_container = policy_container
@@ -125,6 +126,9 @@ class SelfPlayScheduler:
         self.train_autocast = train_autocast
         # the trainer's update captured as one HIP graph and replayed per step (_Trainer graph=True)
         self.train_graph = train_graph
+        # the residual blocks' 3x3 convolutions of the autocast update on the HIP matrix-core kernels
+        # (trainconv.py) instead of MIOpen (_Trainer hip_convs=True)
+        self.train_hip_convs = train_hip_convs
         self.exchange_every = exchange_every  # plies per episode-batch exchange round (distributed.MoveExchange)
         # >1: LanedEngine (arenas on separate HIP streams, each a complete arena); None = 2 lanes for
         # arenas of >= 1,024 games, where the overlap pays (bench.py), else one arena
@@ -207,7 +211,7 @@ class SelfPlayScheduler:
                                 batch_size=kw.get("batch_size", 64), min_memory=kw.get("min_memory", 20000),
                                 q_average=kw.get("q_average", True), device=self.device, W=self.W, H=self.H,
                                 A=self.A, overlap=self._overlap_ok(), autocast=self.train_autocast,
-                                graph=self.train_graph)
+                                graph=self.train_graph, hip_convs=self.train_hip_convs)
         if self.save_dir and self.rank == 0:  # rank 0 owns the replay ring (MoveExchange gathers to it)
             self.trainer.run_dir = os.path.join(self.save_dir, self.start_time)
         if resume_memory and self.rank == 0:  # updateworker.py:67-69 (before the model, as there)
@@ -536,7 +540,7 @@ class _Trainer:
     GRAPH_WARMUP = 3
 
     def __init__(self, network, optim, memory_size, batch_size, min_memory, q_average, device, W=7, H=6, A=7,
-                 train_mode=True, overlap=True, autocast=False, graph=True):
+                 train_mode=True, overlap=True, autocast=False, graph=True, hip_convs=True):
         from .replay import DeviceReplay
 
         dev = torch.device(device) if device is not None else torch.device("cpu")
@@ -555,6 +559,9 @@ class _Trainer:
         # `with autocast(): self.policy.update_from_memory()`, no GradScaler); only on a CUDA device,
         # where the reference's autocast is active (it is a no-op on CPU)
         self.autocast = bool(autocast) and dev.type == "cuda"
+        # under autocast the residual blocks' 3x3 convolutions (forward and backward) run on the HIP
+        # matrix-core kernels (trainconv.py) instead of MIOpen's VALU Winograd kernels
+        self.hip_convs = bool(hip_convs) and self.autocast
         self.scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optim, "max", patience=15, factor=0.5,
                                                                     min_lr=0.00001, cooldown=5)
         self.graph = bool(graph) and dev.type == "cuda"
@@ -631,8 +638,11 @@ class _Trainer:
             torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)
 
     def _train_step(self, s, z, pi, q):
+        from .trainconv import hip_block_convs
+
         self.network.train(self.train_mode)
-        with torch.autocast("cuda", dtype=torch.float16, enabled=self.autocast):
+        with torch.autocast("cuda", dtype=torch.float16, enabled=self.autocast), \
+                hip_block_convs(self.network, self.hip_convs):
             loss = az_loss(self.network, s, z, pi, q, self.q_average)
             self.optim.zero_grad()
             loss.backward()
@@ -671,7 +681,9 @@ class _Trainer:
         self.optim.zero_grad(set_to_none=True)  # the gradients are allocated inside the graph's pool
         # captured on torch's side stream (it synchronises the device once, here); replays run on the
         # caller's current stream
-        with torch.cuda.graph(g):
+        from .trainconv import hip_block_convs
+
+        with torch.cuda.graph(g), hip_block_convs(self.network, self.hip_convs):
             with torch.autocast("cuda", dtype=torch.float16, enabled=self.autocast, cache_enabled=False):
                 loss = az_loss(self.network, *self._g_in, self.q_average)
             loss.backward()

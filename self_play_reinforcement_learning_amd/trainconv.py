@@ -1,0 +1,127 @@
+"""The trainer's 3x3 residual-block convolutions on the HIP matrix-core kernels (csrc/trainconv.hip).
+
+The UpdateWorker trains the ResidualTower under fp16 autocast (updateworker.py:147-149), where every
+`BasicBlock` conv (games/general/modules.py:13-40) is a conv2d of fp16 activations, weights and bias.
+MIOpen runs those as VALU dot2 Winograd kernels (profiles/r04/trainer/); `hip_block_convs(network)`
+routes them -- forward, input gradient and weight / bias gradients -- to spmcts_conv3x3_* instead, for
+the duration of a `with` block (the trainer's step, eager or while a HIP graph is captured).  Nothing
+else of the module changes (no new parameters, the same state_dict), and outside the block the
+module's own nn.Conv2d.forward runs again.
+
+Numerics: fp16 operands, fp32 accumulation, one rounding to fp16 per output (as MIOpen's fp16
+kernels); the weight gradient is summed over board groups in a fixed order, so results are
+deterministic.  Checked against the fp32 torch convolution of the same fp16 operands in
+tests/test_gpu_trainconv.py.
+"""
+import contextlib
+import ctypes
+
+import torch
+
+from . import _lib
+
+_F16 = torch.float16
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def supported(width, height, cin, cout):
+    return bool(_lib.lib().spmcts_conv3x3_supported(int(width), int(height), int(cin), int(cout)))
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise _lib.SpmctsError(f"{what} failed ({rc})")
+
+
+def conv3x3_forward(x, wf, bias, cout):
+    """y = conv(x, w) + bias on the packed forward weights wf [cout][9][cin]; x fp16 [n][cin][W][H]."""
+    n, cin, W, H = x.shape
+    y = torch.empty((n, cout, W, H), dtype=_F16, device=x.device)
+    _check(_lib.lib().spmcts_conv3x3_fwd(n, W, H, cin, cout, _ptr(x), _ptr(wf), _ptr(bias), _ptr(y), _stream()),
+           "spmcts_conv3x3_fwd")
+    return y
+
+
+def pack(w):
+    cout, cin = w.shape[:2]
+    wf = torch.empty((cout, 9, cin), dtype=_F16, device=w.device)
+    wb = torch.empty((cin, 9, cout), dtype=_F16, device=w.device)
+    _check(_lib.lib().spmcts_conv3x3_pack(cin, cout, _ptr(w), _ptr(wf), _ptr(wb), _stream()), "spmcts_conv3x3_pack")
+    return wf, wb
+
+
+def weight_grad(x, dy, bias_grad=True):
+    """(dw fp16 [cout][cin][3][3], db fp16 [cout] or None) of y = conv(x, w) + b for the output grad dy."""
+    n, cin, W, H = x.shape
+    cout = dy.shape[1]
+    tiles = (cout // 32) * (cin // 32)
+    splits = max(1, min(n, 256 // max(1, tiles)))
+    part = torch.empty((splits, cout, 9, cin), dtype=torch.float32, device=x.device)
+    dw = torch.empty((cout, cin, 3, 3), dtype=_F16, device=x.device)
+    db = torch.empty((cout,), dtype=_F16, device=x.device) if bias_grad else None
+    _check(_lib.lib().spmcts_conv3x3_wgrad(n, W, H, cin, cout, _ptr(x), _ptr(dy), _ptr(part), splits, _ptr(dw),
+                                           _ptr(db), _stream()), "spmcts_conv3x3_wgrad")
+    return dw, db
+
+
+class Conv3x3(torch.autograd.Function):
+    """conv2d(x, w, b, stride 1, padding 1) as autocast runs it: every floating input cast to fp16."""
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=_F16)
+    def forward(ctx, x, w, b):
+        if x.dtype != _F16 or w.dtype != _F16:
+            raise TypeError("Conv3x3 runs on fp16 operands (inside torch.autocast)")
+        x = x.contiguous()
+        wf, wb = pack(w.contiguous())
+        bias = None if b is None else b.contiguous()
+        y = conv3x3_forward(x, wf, bias, w.shape[0])
+        ctx.save_for_backward(x, wb)
+        ctx.has_bias = b is not None
+        return y
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, gy):
+        x, wb = ctx.saved_tensors
+        gy = gy.to(_F16).contiguous()
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = conv3x3_forward(gy, wb, None, x.shape[1])
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            gw, gb = weight_grad(x, gy, ctx.has_bias)
+        return gx, gw, gb
+
+
+def _forward(conv, x):
+    return Conv3x3.apply(x, conv.weight, conv.bias)
+
+
+@contextlib.contextmanager
+def hip_block_convs(network, enabled=True):
+    """Within the block, the residual blocks' 3x3 convolutions of `network` (a ResidualTower on a CUDA
+    device, run under fp16 autocast) go through Conv3x3.  Yields whether they do (False: unsupported
+    shape, another module type, or not enabled -- the module's own convolutions run)."""
+    blocks = getattr(network, "residual_blocks", None)
+    convs = [] if blocks is None else [c for blk in blocks for c in (blk.conv1, blk.conv2)]
+    ok = (enabled and convs and all(
+        isinstance(c, torch.nn.Conv2d) and c.kernel_size == (3, 3) and c.stride == (1, 1) and c.padding == (1, 1)
+        and c.groups == 1 and c.dilation == (1, 1) and c.weight.is_cuda for c in convs)
+        and all(supported(network.width, network.height, c.in_channels, c.out_channels) for c in convs))
+    if not ok:
+        yield False
+        return
+    for c in convs:
+        c.forward = (lambda x, c=c: _forward(c, x))
+    try:
+        yield True
+    finally:
+        for c in convs:
+            del c.forward
