@@ -321,9 +321,9 @@ int spmcts_tower_heads_dev(int32_t width, int32_t height, int32_t channels, int3
  *          input-gradient convolution's weights).
  *   _fwd: y [n][cout][W][H] = bias + conv(x [n][cin][W][H], wpk = wf of _pack); bias may be NULL.  The input
  *         gradient is _fwd(dy, wb) with cin and cout swapped and no bias.
- *   _wgrad: dw [cout][cin][3][3] (fp16) = sum over the batch of dy x x-patches, split over `splits` board
- *           groups into part [splits][cout][9][cin] (f32 scratch) and summed in order; db [cout] (fp16, may
- *           be NULL) = sum of dy over the batch and cells.
+ *   _wgrad: dw [cout][cin][3][3] (fp16) = sum over the batch of dy x x-patches, one slice of 8 boards per
+ *           partial sum (splits must be ceil(n / 8)) into part [splits][cout][9][cin] (f32 scratch), summed in
+ *           order; db [cout] (fp16, may be NULL) = sum of dy over the batch and cells.
  * Return 0, -1 bad argument, -2 unsupported shape, -3 launch error. */
 int spmcts_conv3x3_supported(int32_t width, int32_t height, int32_t cin, int32_t cout);
 int spmcts_conv3x3_pack(int32_t cin, int32_t cout, const void *w, void *wf, void *wb, spmcts_stream stream);

@@ -10,7 +10,8 @@
 //   input grad    dx[b][ci][p] = sum_{co,tap} w[co][ci][8 - tap] dy[b][co][p + tap]          (k_conv3x3 on
 //                 the transposed, flipped weights: the same kernel)
 //   weight grad   dw[co][ci][tap] = sum_{b,p} dy[b][co][p] x[b][ci][p + tap]                 (k_conv3x3_wgrad,
-//                 split over boards, then k_conv3x3_reduce sums the splits in a fixed order; + db)
+//                 one slice of 8 boards per workgroup, then k_conv3x3_reduce sums the slices in a fixed
+//                 order; + db)
 //
 // Tensors are the module's own: NCHW fp16 activations [n][c][W][H] (cell p = x H + y), weights
 // [co][ci][3][3]; fp32 accumulation, one rounding to fp16 at the end as MIOpen's fp16 kernels do.
@@ -54,15 +55,30 @@ __global__ __launch_bounds__(128) void k_conv3x3(int W, int H, int cout, const _
                                                  _Float16 *__restrict__ y) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   constexpr int RSB = CIN * 2 + 16;  // row stride: a 16-B pad shifts consecutive rows by 4 banks
+  constexpr int KS = CIN / 32;
   const int b = blockIdx.x, cot = blockIdx.y;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, q = lane >> 4, n = lane & 15;
   const int HP = H + 2, NPR = (W + 2) * HP, ZR = NPR, cells = W * H;
+  // the wave's whole A operand (its 16 output channels' weights, 9 taps x CIN) is loaded first, so the
+  // loads' latency runs under the input staging below instead of under every k-step
+  const int co = cot * 32 + wave * 16 + n;
+  const _Float16 *wrow = wp + (size_t)co * 9 * CIN + 8 * q;
+  f16x8 a[9][KS];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+    for (int k = 0; k < KS; ++k) a[tap][k] = *(const f16x8 *)(wrow + tap * CIN + 32 * k);
   for (int i = tid; i < (NPR + 1) * RSB / 16; i += 128) ((uint4 *)lds)[i] = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
+  // input staging: a thread takes 8 channels of one cell (8 coalesced 2-byte loads across the threads'
+  // cells) and writes them as one 16-byte LDS row piece
   const _Float16 *xb = x + (size_t)b * CIN * cells;
-  for (int i = tid; i < CIN * cells; i += 128) {
-    const int ci = i / cells, p = i - ci * cells, xx = p / H, yy = p - xx * H;
-    *(_Float16 *)(lds + ((xx + 1) * HP + yy + 1) * RSB + ci * 2) = xb[i];
+  for (int i = tid; i < (CIN / 8) * cells; i += 128) {
+    const int g = i / cells, p = i - g * cells, xx = p / H, yy = p - xx * H;
+    f16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = xb[(size_t)(8 * g + j) * cells + p];
+    *(f16x8 *)(lds + ((xx + 1) * HP + yy + 1) * RSB + g * 16) = v;
   }
   __syncthreads();
   int base[NT];
@@ -76,8 +92,6 @@ __global__ __launch_bounds__(128) void k_conv3x3(int W, int H, int cout, const _
   f32x4 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int co = cot * 32 + wave * 16 + n;
-  const _Float16 *wrow = wp + (size_t)co * 9 * CIN + 8 * q;
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
     const int toff = (tap / 3 - 1) * HP + (tap % 3 - 1);
@@ -85,11 +99,9 @@ __global__ __launch_bounds__(128) void k_conv3x3(int W, int H, int cout, const _
 #pragma unroll
     for (int t = 0; t < NT; ++t) roff[t] = (ok[t] ? base[t] + toff : ZR) * RSB + 16 * q;
 #pragma unroll
-    for (int k = 0; k < CIN / 32; ++k) {
-      const f16x8 a = *(const f16x8 *)(wrow + tap * CIN + 32 * k);
+    for (int k = 0; k < KS; ++k)
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = mfma(a, *(const f16x8 *)(lds + roff[t] + 64 * k), acc[t]);
-    }
+      for (int t = 0; t < NT; ++t) acc[t] = mfma(a[tap][k], *(const f16x8 *)(lds + roff[t] + 64 * k), acc[t]);
   }
   // D: lane 16 q + n holds output channels 4 q + r of the wave's 16, cell 16 t + n
 #pragma unroll
@@ -106,57 +118,58 @@ __global__ __launch_bounds__(128) void k_conv3x3(int W, int H, int cout, const _
 }
 
 // ---------------------------------------------------------------------------------------------------------
-// part[s][co][tap][ci] = sum over the boards of split s of sum_p dy[b][co][p] * x[b][ci][p + tap].
-// GEMM over K = the cells of a padded grid (W + 2) x HP8 (HP8 = H + 2 rounded up to 8, so a row of the grid
-// is 16 B and a dx shift is a whole number of 16-B slots): dy is placed on the grid (zero on the border),
-// x three times, shifted by dy - 1 = -1, 0, +1 cells, so every B fragment (8 consecutive grid cells of one
-// channel at shift (dx - 1) HP8) is one aligned 16-B LDS read.  Workgroup = 32 output x 32 input channels x
-// one split of the batch; 4 waves = 2 x 2 sub-tiles of 16 x 16, all 9 taps (9 accumulators each).
-template <int KK>  // k-steps of 32 grid cells per board
-__global__ __launch_bounds__(256) void k_conv3x3_wgrad(int W, int H, int cin, int cout, int bps, int nb,
+// part[s][co][tap][ci] = sum over the 8 boards of slice s of sum_p dy[b][co][p] * x[b][ci][p + tap].
+// The GEMM's K runs over (cell, board): a lane's 8 consecutive k are the slice's 8 boards at one cell, so
+// both operands are stored board-innermost in LDS -- dy as [cell][co][8 boards], x on the zero-bordered
+// padded grid as [(W + 2)(H + 2) rows][ci][8 boards] -- and a tap shift only moves the x row: every
+// fragment is one aligned 16-B LDS read, and the zero border gives the convolution's padding.  A k-step of
+// 32 covers 4 cells (lane quarter q: cell 4 ks + q).  Workgroup = 32 output x 32 input channels x one
+// slice; 4 waves = 2 x 2 sub-tiles of 16 x 16, all 9 taps (9 accumulators each).
+__global__ __launch_bounds__(256) void k_conv3x3_wgrad(int W, int H, int cin, int cout, int nb,
                                                        const _Float16 *__restrict__ x,
                                                        const _Float16 *__restrict__ dy, float *__restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  constexpr int KP = 32 * KK;         // grid cells per board, padded to the k-steps
-  constexpr int DS = KP + 8;          // sdy row (halfs): 16-B multiple
-  constexpr int XS = KP + 24;         // sx row: 8 halfs of margin either side + the 16-B pad
-  _Float16 *sdy = (_Float16 *)lds;                // [32 co][DS]
-  _Float16 *sx = sdy + 32 * DS;                   // [3 dy][32 ci][XS], cell r at index 8 + r
   const int cot = blockIdx.x, cit = blockIdx.y, s = blockIdx.z;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, q = lane >> 4, n = lane & 15;
-  const int HP = (H + 2 + 7) & ~7, cells = W * H;
+  const int HP = H + 2, NPR = (W + 2) * HP, cells = W * H, KSTEPS = (cells + 3) / 4;
+  f16x8 *sdy = (f16x8 *)lds;               // [4 KSTEPS cells][32 co] (cells past W H: zero)
+  f16x8 *sx = sdy + 4 * KSTEPS * 32;       // [NPR + 1 rows][32 ci] (the last row: zero, for those cells)
+  const int ZR = NPR;
+  // zero the padded-grid border, the zero row and the dy cells past W H
+  for (int i = tid; i < (NPR + 1) * 32; i += 256) {
+    const int r = i >> 5, gx = r / HP - 1, gy = r % HP - 1;
+    if (r == ZR || gx < 0 || gx >= W || gy < 0 || gy >= H) sx[i] = f16x8{};
+  }
+  for (int i = cells * 32 + tid; i < 4 * KSTEPS * 32; i += 256) sdy[i] = f16x8{};
+  // the slice's boards, board-innermost: 8 coalesced 2-byte loads (across the threads' cells) per piece
+  const int b0 = s * 8;
+  for (int i = tid; i < 32 * cells; i += 256) {
+    const int c = i / cells, p = i - c * cells, xx = p / H, yy = p - xx * H;
+    f16x8 vd, vx;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int b = b0 + j;
+      const bool in = b < nb;
+      vd[j] = in ? dy[((size_t)b * cout + cot * 32 + c) * cells + p] : (_Float16)0.f;
+      vx[j] = in ? x[((size_t)b * cin + cit * 32 + c) * cells + p] : (_Float16)0.f;
+    }
+    sdy[p * 32 + c] = vd;
+    sx[((xx + 1) * HP + yy + 1) * 32 + c] = vx;
+  }
+  __syncthreads();
   const int cs = wave & 1, is = wave >> 1;  // the wave's co / ci sub-tile of 16
   f32x4 acc[9];
 #pragma unroll
   for (int t = 0; t < 9; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int j = 0; j < bps; ++j) {
-    const int b = s * bps + j;
-    if (b >= nb) break;
-    __syncthreads();  // the previous board's reads are done
-    const _Float16 *dyb = dy + ((size_t)b * cout + cot * 32) * cells;
-    const _Float16 *xb = x + ((size_t)b * cin + cit * 32) * cells;
-    for (int i = tid; i < 32 * DS; i += 256) {
-      const int c = i / DS, r = i - c * DS, gx = r / HP - 1, gy = r % HP - 1;
-      const bool in = r < KP && gx >= 0 && gx < W && gy >= 0 && gy < H;
-      sdy[i] = in ? dyb[(size_t)c * cells + gx * H + gy] : (_Float16)0.f;
-    }
-    for (int i = tid; i < 3 * 32 * XS; i += 256) {
-      const int d = i / (32 * XS), rem = i - d * 32 * XS, c = rem / XS, r = rem - c * XS - 8 + d - 1;
-      // grid cell r + (d - 1); r may run past either end of the grid (margins): zero there
-      const int gx = r >= 0 ? r / HP - 1 : -1, gy = r >= 0 ? r % HP - 1 : -1;
-      const bool in = r >= 0 && r < (W + 2) * HP && gx >= 0 && gx < W && gy >= 0 && gy < H;
-      sx[i] = in ? xb[(size_t)c * cells + gx * H + gy] : (_Float16)0.f;
-    }
-    __syncthreads();
+  for (int ks = 0; ks < KSTEPS; ++ks) {
+    const int p = 4 * ks + q;
+    const f16x8 av = sdy[p * 32 + cs * 16 + n];
+    const bool ok = p < cells;
+    const int r0 = ok ? (p / H + 1) * HP + p % H + 1 : ZR;
 #pragma unroll
-    for (int kk = 0; kk < KK; ++kk) {
-      const f16x8 a = *(const f16x8 *)(sdy + (cs * 16 + n) * DS + 32 * kk + 8 * q);
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int d = tap % 3, dxo = (tap / 3 - 1) * HP;
-        const f16x8 bb = *(const f16x8 *)(sx + (d * 32 + is * 16 + n) * XS + 8 + 32 * kk + 8 * q + dxo);
-        acc[tap] = mfma(a, bb, acc[tap]);
-      }
+    for (int tap = 0; tap < 9; ++tap) {
+      const int r = ok ? r0 + (tap / 3 - 1) * HP + (tap % 3 - 1) : ZR;
+      acc[tap] = mfma(av, sx[r * 32 + is * 16 + n], acc[tap]);
     }
   }
 #pragma unroll
@@ -168,7 +181,7 @@ __global__ __launch_bounds__(256) void k_conv3x3_wgrad(int W, int H, int cin, in
     }
 }
 
-// dw[co][ci][tap] = fp16(sum_s part[s][co][tap][ci]) (splits in order); blocks past the weights: db[co] =
+// dw[co][ci][tap] = fp16(sum_s part[s][co][tap][ci]) (slices in order); blocks past the weights: db[co] =
 // fp16(sum over boards and cells of dy[b][co][p]) in a fixed order (a 256-thread tree per channel)
 __global__ __launch_bounds__(256) void k_conv3x3_reduce(int cin, int cout, int splits, int nb, int cells,
                                                         const float *__restrict__ part, const _Float16 *__restrict__ dy,
@@ -176,12 +189,12 @@ __global__ __launch_bounds__(256) void k_conv3x3_reduce(int cin, int cout, int s
   const int nw = cout * cin * 9;
   const int wblocks = (nw + 255) / 256;
   if ((int)blockIdx.x < wblocks) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int i = blockIdx.x * 256 + threadIdx.x;  // in part's [co][tap][ci] order: coalesced reads
     if (i >= nw) return;
-    const int tap = i % 9, ci = (i / 9) % cin, co = i / (9 * cin);
+    const int ci = i % cin, tap = (i / cin) % 9, co = i / (9 * cin);
     float acc = 0.f;
-    for (int s = 0; s < splits; ++s) acc += part[(((size_t)s * cout + co) * 9 + tap) * cin + ci];
-    dw[i] = (_Float16)acc;
+    for (int s = 0; s < splits; ++s) acc += part[(size_t)s * nw + i];
+    dw[((size_t)co * cin + ci) * 9 + tap] = (_Float16)acc;
     return;
   }
   const int co = blockIdx.x - wblocks;
@@ -201,11 +214,12 @@ __global__ __launch_bounds__(256) void k_conv3x3_reduce(int cin, int cout, int s
   if (threadIdx.x == 0) db[co] = (_Float16)red[0];
 }
 
-// boards of up to 64 cells with H + 2 <= 8 (one 16-B grid row per x in the weight gradient) and an LDS tile of
-// at most 100 padded rows; C in {128, 256} input channels, outputs a multiple of 32
+// boards of up to 64 cells with an LDS tile of at most 100 padded rows (and the weight gradient's dy and x
+// slices within 64 KB of LDS); C in {128, 256} input channels, outputs a multiple of 32
 static bool shape_ok(int W, int H, int cin, int cout) {
-  return W >= 1 && H >= 1 && W * H <= 64 && H + 2 <= 8 && (W + 2) * (H + 2) <= 100 && (cin == 128 || cin == 256) &&
-         cout % 32 == 0 && cout >= 32 && cout <= 1024;
+  const int cells = W * H, npr = (W + 2) * (H + 2);
+  return W >= 1 && H >= 1 && cells <= 64 && npr <= 100 && 4 * ((cells + 3) / 4) + npr + 1 <= 128 &&
+         (cin == 128 || cin == 256) && cout % 32 == 0 && cout >= 32 && cout <= 1024;
 }
 
 template <int CIN, int NT>
@@ -258,31 +272,16 @@ int spmcts_conv3x3_fwd(int32_t n, int32_t width, int32_t height, int32_t cin, in
 int spmcts_conv3x3_wgrad(int32_t n, int32_t width, int32_t height, int32_t cin, int32_t cout, const void *x,
                          const void *dy, float *part, int32_t splits, void *dw, void *db, spmcts_stream stream) {
   if (!tconv::shape_ok(width, height, cin, cout) || cin % 32) return -2;
-  if (!x || !dy || !part || !dw || splits <= 0) return -1;
+  if (!x || !dy || !part || !dw || splits != (n + 7) / 8 || splits <= 0) return -1;
   hipStream_t s = (hipStream_t)stream;
-  const int HP = (height + 2 + 7) & ~7, kk = ((width + 2) * HP + 31) / 32;
-  const int bps = (n + splits - 1) / splits;
-  const size_t lds = (size_t)(32 * (32 * kk + 8) + 3 * 32 * (32 * kk + 24)) * 2;
-  const dim3 grid(cout / 32, cin / 32, splits);
-  if (n > 0) {
-    switch (kk) {
-      case 1: hipLaunchKernelGGL(tconv::k_conv3x3_wgrad<1>, grid, dim3(256), lds, s, width, height, cin, cout, bps, n,
-                                 (const _Float16 *)x, (const _Float16 *)dy, part); break;
-      case 2: hipLaunchKernelGGL(tconv::k_conv3x3_wgrad<2>, grid, dim3(256), lds, s, width, height, cin, cout, bps, n,
-                                 (const _Float16 *)x, (const _Float16 *)dy, part); break;
-      case 3: hipLaunchKernelGGL(tconv::k_conv3x3_wgrad<3>, grid, dim3(256), lds, s, width, height, cin, cout, bps, n,
-                                 (const _Float16 *)x, (const _Float16 *)dy, part); break;
-      case 4: hipLaunchKernelGGL(tconv::k_conv3x3_wgrad<4>, grid, dim3(256), lds, s, width, height, cin, cout, bps, n,
-                                 (const _Float16 *)x, (const _Float16 *)dy, part); break;
-      default: return -2;
-    }
-    if (hipGetLastError() != hipSuccess) return -3;
-  } else {
-    if (hipMemsetAsync(part, 0, (size_t)splits * cout * 9 * cin * sizeof(float), s) != hipSuccess) return -3;
-  }
+  const int cells = width * height, ksteps = (cells + 3) / 4, npr = (width + 2) * (height + 2);
+  const size_t lds = (size_t)(4 * ksteps * 32 + (npr + 1) * 32) * 16;
+  hipLaunchKernelGGL(tconv::k_conv3x3_wgrad, dim3(cout / 32, cin / 32, splits), dim3(256), lds, s, width, height, cin,
+                     cout, n, (const _Float16 *)x, (const _Float16 *)dy, part);
+  if (hipGetLastError() != hipSuccess) return -3;
   const int wblocks = (cout * cin * 9 + 255) / 256;
   hipLaunchKernelGGL(tconv::k_conv3x3_reduce, dim3(wblocks + (db ? cout : 0)), dim3(256), 0, s, cin, cout, splits, n,
-                     width * height, (const float *)part, (const _Float16 *)dy, (_Float16 *)dw, (_Float16 *)db);
+                     cells, (const float *)part, (const _Float16 *)dy, (_Float16 *)dw, (_Float16 *)db);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

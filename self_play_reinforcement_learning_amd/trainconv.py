@@ -61,8 +61,7 @@ def weight_grad(x, dy, bias_grad=True):
     """(dw fp16 [cout][cin][3][3], db fp16 [cout] or None) of y = conv(x, w) + b for the output grad dy."""
     n, cin, W, H = x.shape
     cout = dy.shape[1]
-    tiles = (cout // 32) * (cin // 32)
-    splits = max(1, min(n, 256 // max(1, tiles)))
+    splits = (n + 7) // 8  # one slice of 8 boards per partial sum (trainconv.hip k_conv3x3_wgrad)
     part = torch.empty((splits, cout, 9, cin), dtype=torch.float32, device=x.device)
     dw = torch.empty((cout, cin, 3, 3), dtype=_F16, device=x.device)
     db = torch.empty((cout,), dtype=_F16, device=x.device) if bias_grad else None

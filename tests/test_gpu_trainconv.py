@@ -65,7 +65,7 @@ def test_hip_block_convs_patch_is_scoped():
     from self_play_reinforcement_learning_amd.modules import ResidualTower
     from self_play_reinforcement_learning_amd.trainconv import hip_block_convs
 
-    net = ResidualTower(7, 6, 7, num_blocks=2, filter_factor=32).cuda()
+    net = ResidualTower(7, 6, 7, num_blocks=2, filter_factor=32).cuda().eval()  # no dropout masks
     keys = list(net.state_dict())
     x = torch.randint(-1, 2, (8, 7, 6), device="cuda")
     with torch.autocast("cuda", dtype=torch.float16):
