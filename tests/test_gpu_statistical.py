@@ -162,6 +162,17 @@ def _g6(name):
     return load_json("threaded_stats.json")[name]
 
 
+def _n_positions(name):
+    import json
+    import os
+
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "threaded_stats.json")) as f:
+        return len(json.load(f)[name]["positions"])
+
+
+N_RESNET_POS = _n_positions("resnet_single")  # 6 positions x 4,000 reference searches since round 5
+
+
 def _ref_samples(pos):
     tp = np.array([s["tree_probs"] for s in pos["samples"]], dtype=np.float64)
     act = np.array([s["action"] for s in pos["samples"]])
@@ -250,7 +261,7 @@ def test_threaded_search_matches_reference_table(pi):
     assert ok, info
 
 
-@pytest.mark.parametrize("pi", [0, 1, 2])
+@pytest.mark.parametrize("pi", range(N_RESNET_POS))
 def test_threaded_search_matches_reference_resnet(pi):
     """The headline configuration's search: ResNet-128x20 (the reference's seed-0 init), 200 sims,
     4 sims in flight, against the reference's threaded samples at the stated tolerance; the leaf
@@ -277,26 +288,26 @@ def test_sequential_search_matches_reference_resnet(pi):
 
 # Stated bounds on the fused tower's effect on the bench-mode search (K = 4, Philox, 200 sims,
 # ResNet-128x20): every mean visit fraction within TOL of the fp32-evaluator search on the same Philox
-# streams, and within 4.5 SE + TOL of the reference's own threaded samples (G6 resnet_single, 1,000
-# searches per position).  fp16 (the reference's inference dtype) keeps 11 significand bits; bf16 keeps
-# 8 and moves this net's small values (std 0.037) by ~0.002 (scripts/tower_err.py), 8x fp16's error.
-# Measured (scripts/diag/shift_excess.py, profiles/r04/shift_excess.json; the searches are deterministic:
-# fixed Philox seeds, batch-independent trunk): fp16 moves the mean visit fractions by <= 0.0007 from the
-# fp32-evaluator search, bf16 by up to 0.0157 (G6 position 2); the negative controls lie at max excess
-# over 4.5 SE of 0.0114 / 0.0235 (serial search, fp16 / bf16) and 0.10 (half budget).  Round 3's bf16 bound
-# of 0.03 did not reject the serial search; 0.02 passes bf16 and rejects it.  bf16 is not the headline
-# dtype (bench.py --dtype fp16; --secondary adds a bf16 line on request).
-SHIFT_TOL = {"fp16": 0.01, "bf16": 0.02}
+# streams, and within 4.5 SE + TOL of the reference's own threaded samples (G6 resnet_single: since round 5
+# 4,000 searches at each of 6 positions).  fp16 (the reference's inference dtype) keeps 11 significand bits;
+# bf16 keeps 8 and moves this net's small values (std 0.037) by ~0.002 (scripts/tower_err.py), 8x fp16's
+# error.  Measured (scripts/diag/shift_excess.py, profiles/r04/shift_excess.json and profiles/r05/g6/; the
+# searches are deterministic: fixed Philox seeds, batch-independent trunk): fp16 moves the mean visit
+# fractions by <= 0.0007 from the fp32-evaluator search, bf16 by up to 0.0157 (G6 position 2).  Round 5
+# tightened the fp16 bound 0.01 -> 0.003 (about 4x the measured shift) with 4x the reference samples, so the
+# negative controls (test_resnet_statistical_check_has_power) are rejected by at least twice the bound.
+# bf16 is not the headline dtype (bench.py --dtype fp16; --secondary adds a bf16 line on request).
+SHIFT_TOL = {"fp16": 0.003, "bf16": 0.02}
 
 
 @pytest.mark.parametrize("precision", ["fp16", "bf16"])
-@pytest.mark.parametrize("pi", [0, 1, 2])
+@pytest.mark.parametrize("pi", range(N_RESNET_POS))
 def test_fused_tower_search_shift(pi, precision):
     """The bench's fused tower instead of fp32 leaf evaluation, at the stated SHIFT_TOL."""
     d = _g6("resnet_single")
     pos = d["positions"][pi]
     cp, ca = _ref_samples(pos)
-    assert len(cp) >= 1000
+    assert len(cp) >= (4000 if precision == "fp16" else 1000)
     tol = SHIFT_TOL[precision]
     fp, _, _ = _gpu_threaded(pos["opening"], 4096, d["sims"], d["thread_count"], net=_resnet_evaluator(d))
     bp, ba, _ = _gpu_threaded(pos["opening"], 4096, d["sims"], d["thread_count"], net=_resnet_evaluator(d, precision))
@@ -308,28 +319,47 @@ def test_fused_tower_search_shift(pi, precision):
     assert (np.abs(fc - fg) <= 4.5 * sef + tol).all(), (fc.round(4), fg.round(4))
 
 
+def _control_excess(d, opening_idx, ev, sims, K, alpha=1.0):
+    """max over the actions of |control - reference| - 4.5 SE at one G6 position."""
+    pos = d["positions"][opening_idx]
+    cp, _ = _ref_samples(pos)
+    gp, _, _ = _gpu_threaded(pos["opening"], 4096, sims, K, net=ev, alpha=alpha)
+    se = np.sqrt(cp.var(0, ddof=1) / len(cp) + gp.var(0, ddof=1) / len(gp))
+    return float((np.abs(gp.mean(0) - cp.mean(0)) - 4.5 * se).max())
+
+
 @pytest.mark.parametrize("precision", ["fp16", "bf16"])
 @pytest.mark.parametrize("variant", ["sims100", "serial"])
 def test_resnet_statistical_check_has_power(variant, precision):
     """Negative control at the headline net: the fused-tower comparison at its stated bound (4.5 SE +
-    SHIFT_TOL: 0.01 for fp16, the bench's dtype; 0.02 for bf16, bench.py --dtype bf16 / --secondary)
+    SHIFT_TOL: 0.003 for fp16, the bench's dtype; 0.02 for bf16, bench.py --dtype bf16 / --secondary)
     rejects, against the reference's threaded ResNet samples, a search with half the simulation budget
     (100 instead of 200) and one run serially (1 simulation in flight instead of the reference's
-    thread_count with virtual loss, mcts.py:229-262).  Root noise drawn with Dirichlet alpha 0.3 instead
-    of 1 (mcts.py:135) moved the mean visit fractions of this position by at most 0.004 (measured round 3),
-    inside the 0.01 bound: a difference of that size is below what this check resolves."""
+    thread_count with virtual loss, mcts.py:229-262) -- at fp16 by an excess of at least twice the bound
+    (the check's margin), at the worst of the G6 positions it is run on."""
     d = _g6("resnet_single")
-    pos = d["positions"][2]
-    cp, _ = _ref_samples(pos)
     ev = _resnet_evaluator(d, precision)
-    if variant == "sims100":
-        gp, _, _ = _gpu_threaded(pos["opening"], 4096, 100, d["thread_count"], net=ev)
-    else:
-        gp, _, _ = _gpu_threaded(pos["opening"], 4096, d["sims"], 1, net=ev)
-    se = np.sqrt(cp.var(0, ddof=1) / len(cp) + gp.var(0, ddof=1) / len(gp))
-    dev = np.abs(gp.mean(0) - cp.mean(0)) - 4.5 * se
-    assert not (dev <= SHIFT_TOL[precision]).all(), (gp.mean(0).round(4), cp.mean(0).round(4), se.round(4))
-    print(f"{variant} {precision}: max excess over 4.5 SE {dev.max():.4f} vs bound {SHIFT_TOL[precision]}")
+    sims, K = (100, d["thread_count"]) if variant == "sims100" else (d["sims"], 1)
+    pis = range(N_RESNET_POS) if precision == "fp16" else [2]
+    excess = [_control_excess(d, pi, ev, sims, K) for pi in pis]
+    tol = SHIFT_TOL[precision]
+    print(f"{variant} {precision}: max excess over 4.5 SE per position {np.round(excess, 4).tolist()} vs bound {tol}")
+    assert max(excess) > tol
+    if precision == "fp16":
+        assert max(excess) >= 2 * tol, excess
+
+
+def test_resnet_alpha_control_resolution():
+    """Root noise drawn with Dirichlet alpha 0.3 instead of 1 (mcts.py:135) is a smaller perturbation than the
+    controls above: the test records its excess over 4.5 SE at each G6 position instead of asserting a
+    rejection.  DESIGN.md §1 states the sample size that would resolve it (the shift is ~0.004 per visit
+    fraction; rejecting it at the fp16 bound needs 4.5 SE < 0.004 - 0.003)."""
+    d = _g6("resnet_single")
+    ev = _resnet_evaluator(d, "fp16")
+    excess = [_control_excess(d, pi, ev, d["sims"], d["thread_count"], alpha=0.3) for pi in range(N_RESNET_POS)]
+    print(f"alpha 0.3 fp16: max excess over 4.5 SE per position {np.round(excess, 4).tolist()} vs bound "
+          f"{SHIFT_TOL['fp16']}")
+    assert all(np.isfinite(excess))
 
 
 def test_threaded_statistical_check_has_power():
