@@ -317,13 +317,13 @@ int spmcts_tower_heads_dev(int32_t width, int32_t height, int32_t channels, int3
  * calls that the UpdateWorker's autocast SGD step makes, updateworker.py:141-149 -> mcts.py:254-270 ->
  * modules.py:13-40); fp32 accumulation, deterministic (no atomics).
  *   _supported: 1 if the (board, channels) shape is handled, in both directions (forward and input grad).
- *   _pack: w [cout][cin][3][3] -> wf [cout][9][cin] (forward) and wb [cin][9][cout] (taps flipped: the
- *          input-gradient convolution's weights).
- *   _fwd: y [n][cout][W][H] = bias + conv(x [n][cin][W][H], wpk = wf of _pack); bias may be NULL.  The input
- *         gradient is _fwd(dy, wb) with cin and cout swapped and no bias.
- *   _wgrad: dw [cout][cin][3][3] (fp16) = sum over the batch of dy x x-patches, one slice of 8 boards per
- *           partial sum (splits must be ceil(n / 8)) into part [splits][cout][9][cin] (f32 scratch), summed in
- *           order; db [cout] (fp16, may be NULL) = sum of dy over the batch and cells.
+ *   _pack: the fp32 parameter w [cout][cin][3][3], rounded to fp16 -> wf [cout][9][cin] (forward) and
+ *          wb [cin][9][cout] (taps flipped: the input-gradient convolution's weights).
+ *   _fwd: y [n][cout][W][H] (fp16) = fp16(bias) + conv(x [n][cin][W][H] fp16, wpk = wf of _pack); bias is the
+ *         fp32 parameter or NULL.  The input gradient is _fwd(dy, wb) with cin and cout swapped and no bias.
+ *   _wgrad: dw [cout][cin][3][3] = fp16(sum over the batch of dy x x-patches) stored as f32, one slice of 8
+ *           boards per partial sum (splits must be ceil(n / 8)) into part [splits][cout][9][cin] (f32 scratch),
+ *           summed in order; db [cout] (f32 of the fp16 sum, may be NULL) = sum of dy over the batch and cells.
  * Return 0, -1 bad argument, -2 unsupported shape, -3 launch error. */
 int spmcts_conv3x3_supported(int32_t width, int32_t height, int32_t cin, int32_t cout);
 int spmcts_conv3x3_pack(int32_t cin, int32_t cout, const void *w, void *wf, void *wb, spmcts_stream stream);

@@ -13,8 +13,10 @@
 //                 one slice of 8 boards per workgroup, then k_conv3x3_reduce sums the slices in a fixed
 //                 order; + db)
 //
-// Tensors are the module's own: NCHW fp16 activations [n][c][W][H] (cell p = x H + y), weights
-// [co][ci][3][3]; fp32 accumulation, one rounding to fp16 at the end as MIOpen's fp16 kernels do.
+// Tensors are the module's own: NCHW fp16 activations [n][c][W][H] (cell p = x H + y), the fp32 weight and
+// bias parameters (rounded to fp16 on use, as autocast's casts round them, so no separate cast kernels run);
+// fp32 accumulation, one rounding to fp16 at the end as MIOpen's fp16 kernels do; the weight and bias
+// gradients are the fp16-rounded sums handed back as fp32 (what the cast's backward gives the parameter).
 // Deterministic (no atomics): the same bits every run, inside a captured HIP graph as well.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -31,14 +33,15 @@ __device__ __forceinline__ f32x4 mfma(f16x8 a, f16x8 b, f32x4 c) {
 }
 
 // ---------------------------------------------------------------------------------------------------------
-// weight packing: w [co][ci][3][3] -> wf [co][tap][ci] (forward A operand rows) and wb [ci][tap][co] with the
-// taps flipped (the input-gradient convolution's weights)
-__global__ void k_pack(int cin, int cout, const _Float16 *__restrict__ w, _Float16 *__restrict__ wf,
+// weight packing: the fp32 parameter w [co][ci][3][3], rounded to fp16 as autocast's cast rounds it ->
+// wf [co][tap][ci] (forward A operand rows) and wb [ci][tap][co] with the taps flipped (the input-gradient
+// convolution's weights)
+__global__ void k_pack(int cin, int cout, const float *__restrict__ w, _Float16 *__restrict__ wf,
                        _Float16 *__restrict__ wb) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cout * cin * 9) return;
   const int tap = i % 9, ci = (i / 9) % cin, co = i / (9 * cin);
-  const _Float16 v = w[i];
+  const _Float16 v = (_Float16)w[i];
   wf[((size_t)co * 9 + tap) * cin + ci] = v;
   wb[((size_t)ci * 9 + (8 - tap)) * cout + co] = v;
 }
@@ -51,7 +54,7 @@ __global__ void k_pack(int cin, int cout, const _Float16 *__restrict__ w, _Float
 // channel's weights at the same channels (A operand, from global memory / L2).
 template <int CIN, int NT>
 __global__ __launch_bounds__(128) void k_conv3x3(int W, int H, int cout, const _Float16 *__restrict__ x,
-                                                 const _Float16 *__restrict__ wp, const _Float16 *__restrict__ bias,
+                                                 const _Float16 *__restrict__ wp, const float *__restrict__ bias,
                                                  _Float16 *__restrict__ y) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   constexpr int RSB = CIN * 2 + 16;  // row stride: a 16-B pad shifts consecutive rows by 4 banks
@@ -107,7 +110,7 @@ __global__ __launch_bounds__(128) void k_conv3x3(int W, int H, int cout, const _
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int c = cot * 32 + wave * 16 + 4 * q + r;
-    const float bv = bias ? (float)bias[c] : 0.f;
+    const float bv = bias ? (float)(_Float16)bias[c] : 0.f;  // the fp32 bias as autocast's fp16 cast
     _Float16 *yc = y + ((size_t)b * cout + c) * cells;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -182,10 +185,11 @@ __global__ __launch_bounds__(256) void k_conv3x3_wgrad(int W, int H, int cin, in
 }
 
 // dw[co][ci][tap] = fp16(sum_s part[s][co][tap][ci]) (slices in order); blocks past the weights: db[co] =
-// fp16(sum over boards and cells of dy[b][co][p]) in a fixed order (a 256-thread tree per channel)
+// fp16(sum over boards and cells of dy[b][co][p]) in a fixed order (a 256-thread tree per channel); both
+// stored as fp32 values of the fp16 gradient, which is what autocast's weight cast hands its fp32 parameter
 __global__ __launch_bounds__(256) void k_conv3x3_reduce(int cin, int cout, int splits, int nb, int cells,
                                                         const float *__restrict__ part, const _Float16 *__restrict__ dy,
-                                                        _Float16 *__restrict__ dw, _Float16 *__restrict__ db) {
+                                                        float *__restrict__ dw, float *__restrict__ db) {
   const int nw = cout * cin * 9;
   const int wblocks = (nw + 255) / 256;
   if ((int)blockIdx.x < wblocks) {
@@ -194,7 +198,7 @@ __global__ __launch_bounds__(256) void k_conv3x3_reduce(int cin, int cout, int s
     const int ci = i % cin, tap = (i / cin) % 9, co = i / (9 * cin);
     float acc = 0.f;
     for (int s = 0; s < splits; ++s) acc += part[(size_t)s * nw + i];
-    dw[((size_t)co * cin + ci) * 9 + tap] = (_Float16)acc;
+    dw[((size_t)co * cin + ci) * 9 + tap] = (float)(_Float16)acc;  // fp16 grad, as fp32 (the cast's backward)
     return;
   }
   const int co = blockIdx.x - wblocks;
@@ -211,7 +215,7 @@ __global__ __launch_bounds__(256) void k_conv3x3_reduce(int cin, int cout, int s
     if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
     __syncthreads();
   }
-  if (threadIdx.x == 0) db[co] = (_Float16)red[0];
+  if (threadIdx.x == 0) db[co] = (float)(_Float16)red[0];
 }
 
 // boards of up to 64 cells with an LDS tile of at most 100 padded rows (and the weight gradient's dy and x
@@ -227,7 +231,7 @@ static int launch_fwd(int n, int W, int H, int cout, const void *x, const void *
                       hipStream_t s) {
   const size_t lds = (size_t)((W + 2) * (H + 2) + 1) * (CIN * 2 + 16);
   hipLaunchKernelGGL((k_conv3x3<CIN, NT>), dim3(n, cout / 32), dim3(128), lds, s, W, H, cout, (const _Float16 *)x,
-                     (const _Float16 *)wp, (const _Float16 *)bias, (_Float16 *)y);
+                     (const _Float16 *)wp, (const float *)bias, (_Float16 *)y);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -255,7 +259,7 @@ int spmcts_conv3x3_pack(int32_t cin, int32_t cout, const void *w, void *wf, void
   if (cin <= 0 || cout <= 0 || !w || !wf || !wb) return -1;
   const int total = cin * cout * 9;
   hipLaunchKernelGGL(tconv::k_pack, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, cin, cout,
-                     (const _Float16 *)w, (_Float16 *)wf, (_Float16 *)wb);
+                     (const float *)w, (_Float16 *)wf, (_Float16 *)wb);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -281,7 +285,7 @@ int spmcts_conv3x3_wgrad(int32_t n, int32_t width, int32_t height, int32_t cin, 
   if (hipGetLastError() != hipSuccess) return -3;
   const int wblocks = (cout * cin * 9 + 255) / 256;
   hipLaunchKernelGGL(tconv::k_conv3x3_reduce, dim3(wblocks + (db ? cout : 0)), dim3(256), 0, s, cin, cout, splits, n,
-                     cells, (const float *)part, (const _Float16 *)dy, (_Float16 *)dw, (_Float16 *)db);
+                     cells, (const float *)part, (const _Float16 *)dy, (float *)dw, (float *)db);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -41,7 +41,8 @@ def _check(rc, what):
 
 
 def conv3x3_forward(x, wf, bias, cout):
-    """y = conv(x, w) + bias on the packed forward weights wf [cout][9][cin]; x fp16 [n][cin][W][H]."""
+    """y = conv(x, w) + fp16(bias) on the packed forward weights wf [cout][9][cin]; x fp16 [n][cin][W][H],
+    bias the fp32 parameter (or None)."""
     n, cin, W, H = x.shape
     y = torch.empty((n, cout, W, H), dtype=_F16, device=x.device)
     _check(_lib.lib().spmcts_conv3x3_fwd(n, W, H, cin, cout, _ptr(x), _ptr(wf), _ptr(bias), _ptr(y), _stream()),
@@ -50,6 +51,8 @@ def conv3x3_forward(x, wf, bias, cout):
 
 
 def pack(w):
+    """The fp32 weight parameter, rounded to fp16, as (wf [cout][9][cin], wb [cin][9][cout] taps flipped)."""
+    w = w.detach().float().contiguous()
     cout, cin = w.shape[:2]
     wf = torch.empty((cout, 9, cin), dtype=_F16, device=w.device)
     wb = torch.empty((cin, 9, cout), dtype=_F16, device=w.device)
@@ -58,29 +61,31 @@ def pack(w):
 
 
 def weight_grad(x, dy, bias_grad=True):
-    """(dw fp16 [cout][cin][3][3], db fp16 [cout] or None) of y = conv(x, w) + b for the output grad dy."""
+    """(dw [cout][cin][3][3], db [cout] or None) of y = conv(x, w) + b for the output grad dy: the fp16-rounded
+    sums as fp32 tensors (the gradient autocast's fp16 cast hands back to its fp32 parameters)."""
     n, cin, W, H = x.shape
     cout = dy.shape[1]
     splits = (n + 7) // 8  # one slice of 8 boards per partial sum (trainconv.hip k_conv3x3_wgrad)
     part = torch.empty((splits, cout, 9, cin), dtype=torch.float32, device=x.device)
-    dw = torch.empty((cout, cin, 3, 3), dtype=_F16, device=x.device)
-    db = torch.empty((cout,), dtype=_F16, device=x.device) if bias_grad else None
+    dw = torch.empty((cout, cin, 3, 3), dtype=torch.float32, device=x.device)
+    db = torch.empty((cout,), dtype=torch.float32, device=x.device) if bias_grad else None
     _check(_lib.lib().spmcts_conv3x3_wgrad(n, W, H, cin, cout, _ptr(x), _ptr(dy), _ptr(part), splits, _ptr(dw),
                                            _ptr(db), _stream()), "spmcts_conv3x3_wgrad")
     return dw, db
 
 
 class Conv3x3(torch.autograd.Function):
-    """conv2d(x, w, b, stride 1, padding 1) as autocast runs it: every floating input cast to fp16."""
+    """conv2d(x, w, b, stride 1, padding 1) as autocast runs it: x, w and b rounded to fp16, fp16 output.
+    The weight and bias parameters are read in their own dtype (fp32) and rounded inside the kernels, so the
+    two cast kernels autocast runs per parameter and direction do not run."""
 
     @staticmethod
-    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=_F16)
+    @torch.amp.custom_fwd(device_type="cuda")
     def forward(ctx, x, w, b):
-        if x.dtype != _F16 or w.dtype != _F16:
-            raise TypeError("Conv3x3 runs on fp16 operands (inside torch.autocast)")
-        x = x.contiguous()
-        wf, wb = pack(w.contiguous())
-        bias = None if b is None else b.contiguous()
+        ctx.dtypes = (x.dtype, w.dtype, None if b is None else b.dtype)
+        x = x.to(_F16).contiguous()
+        wf, wb = pack(w)
+        bias = None if b is None else b.detach().float().contiguous()
         y = conv3x3_forward(x, wf, bias, w.shape[0])
         ctx.save_for_backward(x, wb)
         ctx.has_bias = b is not None
@@ -90,12 +95,15 @@ class Conv3x3(torch.autograd.Function):
     @torch.amp.custom_bwd(device_type="cuda")
     def backward(ctx, gy):
         x, wb = ctx.saved_tensors
+        xt, wt, bt = ctx.dtypes
         gy = gy.to(_F16).contiguous()
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            gx = conv3x3_forward(gy, wb, None, x.shape[1])
+            gx = conv3x3_forward(gy, wb, None, x.shape[1]).to(xt)
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
             gw, gb = weight_grad(x, gy, ctx.has_bias)
+            gw = gw.to(wt)
+            gb = None if gb is None else gb.to(bt)
         return gx, gw, gb
 
 
