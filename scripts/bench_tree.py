@@ -10,6 +10,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
@@ -22,6 +23,8 @@ def main():
     ap.add_argument("--threads", type=int, default=4)
     ap.add_argument("--plies", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--blocks-per-tree", type=int, default=0,
+                    help="node store per tree (0 = the worst case, no recycling; below it k_compact recycles)")
     args = ap.parse_args()
     import torch
 
@@ -31,7 +34,7 @@ def main():
 
     G, K = args.games, args.threads
     a = Arena("connect4", n_trees=2 * G, n_games=G, iterations=args.sims, rng="philox", seed=5, leaf_format="f32",
-              search_threads=K)
+              search_threads=K, blocks_per_tree=args.blocks_per_tree)
     a.games_set_limit(-1)
     a.games_start(list(range(G)))
     steps = -(-args.sims // K)
@@ -64,8 +67,12 @@ def main():
     for _ in range(args.warmup):
         ply(False)
     c0 = a.counters()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
     for _ in range(args.plies):
         ply(True)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
     a.check()
     c1 = a.counters()
     sims = c1["sims"] - c0["sims"]
@@ -78,7 +85,8 @@ def main():
                expand_dispatches=te.count(), select_avg_us=t_s / max(1, ts.count()) * 1e3,
                expand_avg_us=t_e / max(1, te.count()) * 1e3, tree_bytes=sel_b + exp_b,
                achieved_gbs=(sel_b + exp_b) / ((t_s + t_e) / 1e3) / 1e9, mean_levels=levels / max(1, sims),
-               nn_leaves=nn, sims_done=sims)
+               nn_leaves=nn, sims_done=sims, blocks_per_tree=a.blocks_per_tree, ply_ms=wall / args.plies * 1e3,
+               compactions=c1["compactions"] - c0["compactions"], blocks_in_use_max=c1["blocks_in_use_max"])
     out["frac_of_8tbs"] = out["achieved_gbs"] / 8000.0
     print(json.dumps(out), flush=True)
 

@@ -742,6 +742,7 @@ enum { SIM_DONE = 0, SIM_PENDING = 1, SIM_LEAK = 2, SIM_ERROR = -1 };
 // same arithmetic), so depth 0 reads no memory.
 struct TreeRoot {
   int node, cb, player, n, vl;
+  double w;  // the root's w (terminal backups write it from here, no read-modify-write)
   Board b;
   int cn, cc, cvl;
   double cw;
@@ -759,6 +760,7 @@ __device__ __forceinline__ TreeRoot load_root(const View &v, int tree) {
   R.player = v.rplayer[tree];
   R.n = nd_n<P>(v, nb + R.node);
   R.vl = nd_vl<P>(v, nb + R.node);
+  R.w = nd_w<P>(v, nb + R.node);
   R.cb = nd_c<P>(v, nb + R.node);
   const int lane = threadIdx.x & (P - 1);
   R.cn = 0;
@@ -781,16 +783,42 @@ __device__ __forceinline__ TreeRoot load_root(const View &v, int tree) {
   return R;
 }
 
+// The path of the sim in flight, in LDS (one group per tree): node ids and, per level, the node's n, vl
+// (this sim's virtual loss included) and w as this sim read them.  One wave owns the tree, so nothing changes
+// them between the read and this sim's backup: a terminal backup writes n + 1, w + value, vl - 1 from here
+// instead of reading the nodes again (one memory round trip less per terminal sim).
+struct PathLds {
+  int32_t *node, *n, *vl;
+  double *w;
+};
+// The tree's counters of one kernel launch (the same value in every lane of the group), added to the
+// arena's counters once at the end of the launch instead of a read-modify-write per sim.
+struct SimCnt {
+  int64_t sims = 0, depth = 0, term = 0, leak = 0, nn = 0, hwm = 0;
+  __device__ void flush(int64_t *cnt) const {
+    cnt[C_SIMS] += sims;
+    cnt[C_DEPTH] += depth;
+    cnt[C_TERM] += term;
+    cnt[C_LEAK] += leak;
+    cnt[C_NN] += nn;
+    cnt[C_HWM] = max(cnt[C_HWM], hwm);
+  }
+};
+// sim_vl's result for a terminal leaf among the root's children: the sim read no memory (depth 0 scores
+// from registers) and wrote only the root's record and its child's, which no later sim of this launch
+// reads from memory before the fill's closing fence -- so the next sim needs no fence first.
+enum { SIM_DONE_ROOT = 3 };
+
 // One search_node with virtual loss (mcts.py:340-367) for pending slot j of `tree`, run by the
 // tree's P-lane group.  vl += 1 on every node passed (mcts.py:345), children scored with
 // q = (w - vl)/(n + vl) and u = c p sqrt(N + vl_parent)/(1 + n + vl) (mcts.py:59-78), pending leaves
 // locked (child-block index -2, score -1e10, mcts.py:86-88).  Returns SIM_PENDING with the leaf
-// locked and its path stashed in slot j, SIM_DONE for a terminal leaf (backed up, path vl removed),
-// SIM_LEAK for a leak, SIM_ERROR on a corrupt tree; R (the root in registers) is updated to match.
-// The return value is uniform across the group.
+// locked and its path stashed in slot j, SIM_DONE (SIM_DONE_ROOT at depth 0) for a terminal leaf (backed
+// up, path vl removed), SIM_LEAK for a leak, SIM_ERROR on a corrupt tree; R (the root in registers) is
+// updated to match.  The return value is uniform across the group.
 template <class G>
-__device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng, bool &terr, int32_t *s_node,
-                      bool noise, double nz, int64_t *cnt) {
+__device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng, bool &terr, const PathLds &pl,
+                      bool noise, double nz, SimCnt &sc) {
   constexpr int P = G::APAD;
   const int lane = threadIdx.x & (P - 1);
   const int gbase = (threadIdx.x & 63) & ~(P - 1);
@@ -802,13 +830,17 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
   int player = R.player;
   int node_n = R.n;
   int node_vl = R.vl + 1;  // this sim's virtual loss on the node (mcts.py:345)
+  double node_w = R.w;
   int cb = R.cb;
   R.vl += 1;
   int depth = 0;
   int a0 = 0;  // the root child this sim took (path node 1)
   for (;;) {
     if (lane == 0) {
-      s_node[depth] = node;
+      pl.node[depth] = node;
+      pl.n[depth] = node_n;
+      pl.vl[depth] = node_vl;
+      pl.w[depth] = node_w;
       nd_vl<P>(v, nb + node) = node_vl;
     }
     if (depth == 1 && lane == a0) R.cvl = node_vl;  // the root child's vl, in registers too
@@ -854,7 +886,7 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
       score = (player > 0 ? q : -q) + u;
     }
     if (!group_or<P>(valid ? 1 : 0)) {  // mcts.py:349-354: return, virtual loss left in place
-      if (lane == 0) cnt[C_LEAK] += 1;
+      sc.leak += 1;
       return SIM_LEAK;
     }
     terr = terr || terr_j;  // (a leak consumes no draw, so its tape check does not count)
@@ -866,6 +898,7 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
     const int cc_a = __shfl(cc, gbase + a, 64);
     const int cn_a = __shfl(cn, gbase + a, 64);
     const int cvl_a = __shfl(cvl, gbase + a, 64);
+    const double cw_a = __shfl(cw, gbase + a, 64);
     const int child = cb * P + a;
     if (cc_a < 0) {
       // leaf: _expand_node (mcts.py:301-321)
@@ -874,23 +907,24 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
       const int st = step<G>(nb2, a, player, &rew, &done);
       if (done) {
         // terminal: backup (mcts.py:94-98) then remove the path's virtual loss (:365); one lane per
-        // path node (s_node was written by lane 0 of this wave: LDS operations of a wave stay in order)
+        // path node, the values this sim read (pl: written by lane 0 of this wave, LDS stays in order)
         const double val = terminal_value(v, tree, b, rew * player);
         const bool strong = v.tstrong[tree] != 0;
         for (int k = lane; k <= depth; k += P) {
-          const size_t idx = nb + s_node[k];
-          nd_n<P>(v, idx) += 1;
-          nd_w<P>(v, idx) += val;
+          const size_t idx = nb + pl.node[k];
+          nd_n<P>(v, idx) = pl.n[k] + 1;
+          nd_w<P>(v, idx) = pl.w[k] + val;
           if (strong) nd_f<P>(v, idx) = 1;
-          nd_vl<P>(v, idx) -= 1;
+          nd_vl<P>(v, idx) = pl.vl[k] - 1;
         }
         if (lane == 0) {
-          nd_n<P>(v, nb + child) += 1;
-          nd_w<P>(v, nb + child) += val;
+          nd_n<P>(v, nb + child) = cn_a + 1;
+          nd_w<P>(v, nb + child) = cw_a + val;
           if (strong) nd_f<P>(v, nb + child) = 1;
         }
-        R.n += 1;  // the root is s_node[0]
+        R.n += 1;  // the root is path node 0
         R.vl -= 1;
+        R.w += val;
         if (depth >= 1 && lane == a0) {  // path node 1, the root child a0
           R.cn += 1;
           R.cw += val;
@@ -900,17 +934,16 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
           R.cn += 1;
           R.cw += val;
         }
+        sc.term += 1;
       } else {
         const size_t pb = (size_t)ps * G::MAXD;
-        for (int k = lane; k <= depth; k += P) v.pnode[pb + k] = s_node[k];
+        for (int k = lane; k <= depth; k += P) v.pnode[pb + k] = pl.node[k];
       }
+      sc.sims += 1;
+      sc.depth += depth + 1;
       if (lane == 0) {
         if (st != STEP_OK) set_err(v, SPMCTS_ERR_STATE);
-        cnt[C_SIMS] += 1;
-        cnt[C_DEPTH] += depth + 1;
-        if (done) {
-          cnt[C_TERM] += 1;
-        } else {
+        if (!done) {
           // lock the leaf (mcts.py:359); the path was stashed above for the backup
           nd_c<P>(v, nb + child) = -2;
           v.plen[ps] = depth + 1;
@@ -922,13 +955,14 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
         }
       }
       if (!done && depth == 0 && lane == a) R.cc = -2;
-      return done ? SIM_DONE : SIM_PENDING;
+      return done ? (depth == 0 ? SIM_DONE_ROOT : SIM_DONE) : SIM_PENDING;
     }
     if (depth == 0) a0 = a;
     play<G>(b, a, player);
     node = child;
     node_n = cn_a;
     node_vl = cvl_a + 1;
+    node_w = cw_a;
     cb = cc_a;
     player = -player;
     ++depth;
@@ -943,15 +977,22 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
 // search_node calls is spent (`started` counts them, mcts.py:328-331 submits `iterations`).
 template <class G>
 __device__ int fill_slot_vl(const View &v, int tree, int j, int limit, int &started, TreeRoot &R, TreeRng &rng,
-                            bool &terr, int32_t *s_node, bool noise, double nz, int64_t *cnt) {
+                            bool &terr, const PathLds &pl, bool noise, double nz, SimCnt &sc) {
+  bool unfenced = false;
   while (started < limit) {
     ++started;
-    const int r = sim_vl<G>(v, tree, j, R, rng, terr, s_node, noise, nz, cnt);
+    const int r = sim_vl<G>(v, tree, j, R, rng, terr, pl, noise, nz, sc);
+    if (r == SIM_DONE_ROOT) {  // read nothing, wrote the root and a root child: no fence needed yet
+      unfenced = true;
+      continue;
+    }
     // the next sim reads what this one wrote (lane 0's stores, other lanes' loads): one wave owns
     // the tree, so a workgroup-scope fence (stores complete, same CU's L1) is enough
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    unfenced = false;
     if (r == SIM_PENDING || r == SIM_ERROR) return r;
   }
+  if (unfenced) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // before the next backup's reads
   return SIM_DONE;
 }
 
@@ -960,9 +1001,11 @@ template <class G, int TB = 64>
 __global__ __launch_bounds__(TB) void k_select_vl(View v, int n_active) {
   constexpr int P = G::APAD;
   constexpr int GPB = TB / P;
-  __shared__ int32_t s_node[GPB][G::MAXD];
+  __shared__ int32_t s_node[GPB][G::MAXD], s_n[GPB][G::MAXD], s_vl[GPB][G::MAXD];
+  __shared__ double s_w[GPB][G::MAXD];
   const int lane = threadIdx.x & (P - 1);
   const int grp = threadIdx.x / P;
+  const PathLds pl{s_node[grp], s_n[grp], s_vl[grp], s_w[grp]};
   const int slot = blockIdx.x * (int)(blockDim.x / P) + grp;  // blockDim = 64 (GPB trees) or P (one tree)
   if (slot >= n_active) return;
   const int tree = v.active[slot];
@@ -976,13 +1019,14 @@ __global__ __launch_bounds__(TB) void k_select_vl(View v, int n_active) {
   rng_load(v, tree, rng);
   TreeRoot R = load_root<G>(v, tree);
   bool terr = false;
-  int64_t *cnt = v.cnt + (size_t)tree * C_NCNT;
+  SimCnt sc;
   const int kt = v.tK[tree];  // this tree's sims in flight (its own thread_count, <= K)
   for (int j = 0; j < kt; ++j) {
     if (v.need[tree * v.K + j]) continue;
-    if (fill_slot_vl<G>(v, tree, j, limit, started, R, rng, terr, s_node[grp], noise, nz, cnt) == SIM_ERROR) return;
+    if (fill_slot_vl<G>(v, tree, j, limit, started, R, rng, terr, pl, noise, nz, sc) == SIM_ERROR) return;
   }
   if (lane == 0) {
+    sc.flush(v.cnt + (size_t)tree * C_NCNT);
     v.tstarted[tree] = started;
     if (terr) set_err(v, SPMCTS_ERR_TAPE);
     rng_store(v, tree, rng);
@@ -1283,7 +1327,8 @@ __device__ __forceinline__ void expand_vl_body(View v, const float *probs0, cons
   constexpr int P = G::APAD;
   constexpr int GPB = TB / P;
   constexpr int KMAX = P;  // slots whose records one lane each prefetches (spmcts_arena_create: K <= P)
-  __shared__ int32_t s_node[GPB][G::MAXD];
+  __shared__ int32_t s_node[GPB][G::MAXD], s_n[GPB][G::MAXD], s_vl[GPB][G::MAXD];
+  __shared__ double s_w[GPB][G::MAXD];
   // the prefetched path nodes (k < P) and network outputs of each slot, per tree group; each LDS word
   // is written and later read by the same wave (LDS operations of a wave stay in order)
   __shared__ int32_t s_pnode[GPB][KMAX][P];
@@ -1294,6 +1339,7 @@ __device__ __forceinline__ void expand_vl_body(View v, const float *probs0, cons
   const int gbase = (threadIdx.x & 63) & ~(P - 1);
   const int tree = (blockIdx.x * blockDim.x + threadIdx.x) / P;
   if (tree >= v.T) return;
+  const PathLds pl{s_node[grp], s_n[grp], s_vl[grp], s_w[grp]};
   const int K = v.K;
   const size_t nb = nbase<G>(v, tree);
   const size_t bb = (size_t)tree * v.cap;
@@ -1347,7 +1393,7 @@ __device__ __forceinline__ void expand_vl_body(View v, const float *probs0, cons
     }
   }
   bool terr = false;
-  int64_t *cnt = v.cnt + (size_t)tree * C_NCNT;
+  SimCnt sc;
   // one copy of the slot body (a rolled loop: the unrolled form was 70 KB of code, more than the
   // instruction cache two CUs share, for a kernel that runs one wave per CU on a latency chain)
 #pragma unroll 1
@@ -1387,12 +1433,13 @@ __device__ __forceinline__ void expand_vl_body(View v, const float *probs0, cons
         nd_w<P>(v, nb + leaf) += val;
         v.used[tree] = blk + 1;
         v.need[ps] = 0;
-        cnt[C_NN] += 1;
-        cnt[C_HWM] = max(cnt[C_HWM], (int64_t)(blk + 1));
       }
+      sc.nn += 1;
+      sc.hwm = max(sc.hwm, (int64_t)(blk + 1));
       if (refill && plen > 0) {  // the root is the path's first node
         R.n += 1;
         R.vl -= 1;
+        R.w += val;
       }
       if (refill && plen > 1) {  // path node 1 is a root child: its copy in registers
         if (lane == s_pnode[grp][j][1] - R.cb * P) {
@@ -1408,11 +1455,11 @@ __device__ __forceinline__ void expand_vl_body(View v, const float *probs0, cons
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-      if (refill &&
-          fill_slot_vl<G>(v, tree, j, limit, started, R, rng, terr, s_node[grp], noise, nz, cnt) == SIM_ERROR)
+      if (refill && fill_slot_vl<G>(v, tree, j, limit, started, R, rng, terr, pl, noise, nz, sc) == SIM_ERROR)
         return;
     }
   }
+  if (lane == 0) sc.flush(v.cnt + (size_t)tree * C_NCNT);
   if (refill && lane == 0) {
     v.tstarted[tree] = started;
     if (terr) set_err(v, SPMCTS_ERR_TAPE);
