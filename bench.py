@@ -43,11 +43,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 TRAFFIC_FILE = os.path.join(HERE, "profiles", "r01_bench_prof", "k_tower_traffic.json")  # --search-threads 1
-TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r04_bench_prof", "k_tower_traffic.json")  # 4 (default)
-TREE_TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r04_tree_pmc", "tree_traffic.json")
+TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r05_bench_prof", "k_tower_traffic.json")  # 4 (default)
+TREE_TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r05_tree_pmc", "tree_traffic.json")
 # in-bench clock and MFMA-busy share of the timed k_tower_dyn dispatches (one PMC pass per trunk dtype,
 # scripts/gpu_prof_r04.sh -> scripts/tower_util.py): the roofline's frac = busy x clock / 2.4 GHz / 0.833
-CLOCK_FILES = {d: os.path.join(HERE, "profiles", "r04_bench_prof", f"tower_util_bench_{d}.json") for d in ("fp16", "bf16")}
+CLOCK_FILES = {d: os.path.join(HERE, "profiles", "r05_bench_prof", f"tower_util_bench_{d}.json") for d in ("fp16", "bf16")}
 
 # MI355X reference figures (/opt/skills/guides/MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
