@@ -135,9 +135,10 @@ def test_trainer_snapshots_every_50000_and_at_epoch_end(tmp_path):
     t.rows_added()
     assert files()[0].endswith(":120000")
     first = files()[0]
-    saved = t.save_memory()  # the epoch-end snapshot
-    assert files() == [os.path.basename(saved)] and saved.endswith(":120000") and first != files()[0] or True
-    assert len(files()) == 1
+    saved = t.save_memory()  # the epoch-end snapshot: a new file, the previous one removed
+    assert saved.endswith(":120000") and files() == [os.path.basename(saved)]
+    assert os.path.basename(saved) == first or not (tmp_path / first).exists()
+    assert not (tmp_path / ".memory.partial").exists()
 
 
 def test_scheduler_resume_memory(tmp_path):
