@@ -23,8 +23,19 @@
 
 namespace m16 {
 
-// byte offset, within a row, of the physical 16-channel run of lane quarter q in channel half cg
-__device__ __forceinline__ int run_off(int cg, int q) { return (64 * cg + 16 * q) * 2; }
+// 16-channel output tiles per wave: 4 with the 2 x 2 wave plan (channel halves x row halves, the product
+// trunk), 2 with 4 x 1 (channel quarters x all rows, A/B code 1640)
+template <class K>
+constexpr int MM = K::C / 16 / K::CG;
+
+// byte offset, within a row, of the physical run of lane quarter q for the wave's channel group cg: the
+// wave's 16-channel tiles ct = MM cg + mm sit at 64 (ct / 4) + 16 q + 4 (ct % 4) + r (phys16), so its MM tiles
+// are one run of 4 MM halfs (32 B for MM = 4, 16 B for MM = 2)
+template <class K>
+__device__ __forceinline__ int run_off(int cg, int q) {
+  const int ct0 = MM<K> * cg;
+  return (64 * (ct0 / 4) + 16 * q + 4 * (ct0 % 4)) * 2;
+}
 
 // Which of a 32-row tile's rows MFMA column n of fragment h (0, 1) stands for: row lane_row(n) + h.
 // A B-fragment ds_read_b128 is serviced in 16-lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32)
@@ -62,11 +73,12 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 // One tap of a layer: KK32 k-steps of 32 input channels; B fragments one k-step ahead (the next tap's
 // first ones from its own rows), the weight ring DEPTH k-steps ahead and on into the next layer.
 template <class K, int KK32, int DEPTH, int MG_, int TAP>
-__device__ __forceinline__ void conv_tap(const char *src, const Nbr<K> &nb, f32x4 (&acc)[4][K::NT][2],
+__device__ __forceinline__ void conv_tap(const char *src, const Nbr<K> &nb, f32x4 (&acc)[MM<K>][K::NT][2],
                                          bf16x8 (&bc)[K::NT][2], bf16x8 (&bn)[K::NT][2], int (&off_cur)[K::NT][2],
-                                         int (&off_nxt)[K::NT][2], bf16x8 (&a)[DEPTH][4], int qoff, int rb,
+                                         int (&off_nxt)[K::NT][2], bf16x8 (&a)[DEPTH][MM<K>], int qoff, int rb,
                                          const WBuf &wb, uint32_t wl_off, uint32_t wn_off, int wn_steps) {
   using X = XLive<K, MG_>;
+  constexpr int NM = MM<K>;
   constexpr uint32_t MSTRIDE = 9u * KK32 * 1024u;  // bytes between a wave's 16-channel tiles
   constexpr int STEPS = 9 * KK32;
   constexpr uint32_t LV = X::lt(TAP);
@@ -103,26 +115,26 @@ __device__ __forceinline__ void conv_tap(const char *src, const Nbr<K> &nb, f32x
         }
     }
     const int slot = k % DEPTH;
-    bf16x8 acur[4];
+    bf16x8 acur[NM];
 #pragma unroll
-    for (int mm = 0; mm < 4; ++mm) acur[mm] = a[slot][mm];
+    for (int mm = 0; mm < NM; ++mm) acur[mm] = a[slot][mm];
     const int sn = s + DEPTH;
     if (sn < STEPS) {
 #pragma unroll
-      for (int mm = 0; mm < 4; ++mm) a[slot][mm] = wb.load(wl_off + mm * MSTRIDE + (uint32_t)sn * 1024u);
+      for (int mm = 0; mm < NM; ++mm) a[slot][mm] = wb.load(wl_off + mm * MSTRIDE + (uint32_t)sn * 1024u);
     } else if (kRingAlways || sn - STEPS < wn_steps) {
 #pragma unroll
-      for (int mm = 0; mm < 4; ++mm) a[slot][mm] = wb.load(wn_off + mm * MSTRIDE + (uint32_t)(sn - STEPS) * 1024u);
+      for (int mm = 0; mm < NM; ++mm) a[slot][mm] = wb.load(wn_off + mm * MSTRIDE + (uint32_t)(sn - STEPS) * 1024u);
     }
 #pragma unroll
     for (int t = 0; t < K::NT; ++t)
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int mm = 0; mm < 4; ++mm)
+        for (int mm = 0; mm < NM; ++mm)
           if ((LV >> t) & 1u)
             acc[mm][t][h] = mfma16<K>(acur[mm], bc[t][h], (TAP == 0 && k == 0) ? f32x4{} : acc[mm][t][h]);
-    // one operand read or weight load per MFMA gap: 2 NTA LDS reads and 4 weight loads among 8 NTA MFMAs
+    // one operand read or weight load per MFMA gap: 2 NTA LDS reads and NM weight loads among 2 NM NTA MFMAs
     // (A/B: Cfg ABL 256 leaves the order to the compiler)
     if constexpr (!(K::ABL & 256)) {
 #pragma unroll
@@ -131,11 +143,11 @@ __device__ __forceinline__ void conv_tap(const char *src, const Nbr<K> &nb, f32x
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NM; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
       __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 8 * NTA - 2 * NTA - 4, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 2 * NM * NTA - 2 * NTA - NM, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -153,26 +165,27 @@ __device__ __forceinline__ void conv_tap(const char *src, const Nbr<K> &nb, f32x
 
 // out = relu(acc + bias (+ the block input at the same physical positions, RESID)), into dst.
 template <class K, bool RESID>
-__device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][K::NT][2], char *dst, const float4 (&bv)[4], int cg,
-                                         int mg, int q, int rb) {
+__device__ __forceinline__ void epilogue(const f32x4 (&acc)[MM<K>][K::NT][2], char *dst, const float4 (&bv)[MM<K>],
+                                         int cg, int mg, int q, int rb) {
+  constexpr int NM = MM<K>, NU = NM / 2;  // the run: NU 16-byte pieces
 #pragma unroll
   for (int t = 0; t < K::NT; ++t) {
-    uint4 res[2][2];
+    uint4 res[2][NU];
     if constexpr (RESID) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const char *p = dst + ((mg * K::NT + t) * 32 + rb + h) * K::RS + run_off(cg, q);
-        res[h][0] = *(const uint4 *)p;
-        res[h][1] = *(const uint4 *)(p + 16);
+        const char *p = dst + ((mg * K::NT + t) * 32 + rb + h) * K::RS + run_off<K>(cg, q);
+#pragma unroll
+        for (int u = 0; u < NU; ++u) res[h][u] = *(const uint4 *)(p + 16 * u);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      char *p = dst + ((mg * K::NT + t) * 32 + rb + h) * K::RS + run_off(cg, q);
-      uint32_t o[8];
+      char *p = dst + ((mg * K::NT + t) * 32 + rb + h) * K::RS + run_off<K>(cg, q);
+      uint32_t o[2 * NM];
 #pragma unroll
-      for (int mm = 0; mm < 4; ++mm) {
+      for (int mm = 0; mm < NM; ++mm) {
         // physical 4 mm + r within the run: output channel 16 mm + 4 q + r
         float v0 = acc[mm][t][h][0] + bv[mm].x, v1 = acc[mm][t][h][1] + bv[mm].y;
         float v2 = acc[mm][t][h][2] + bv[mm].z, v3 = acc[mm][t][h][3] + bv[mm].w;
@@ -187,27 +200,28 @@ __device__ __forceinline__ void epilogue(const f32x4 (&acc)[4][K::NT][2], char *
         o[2 * mm] = K::relu_pk(f32x2{v0, v1});
         o[2 * mm + 1] = K::relu_pk(f32x2{v2, v3});
       }
-      *(uint4 *)p = make_uint4(o[0], o[1], o[2], o[3]);
-      *(uint4 *)(p + 16) = make_uint4(o[4], o[5], o[6], o[7]);
+#pragma unroll
+      for (int u = 0; u < NU; ++u) *(uint4 *)(p + 16 * u) = make_uint4(o[4 * u], o[4 * u + 1], o[4 * u + 2], o[4 * u + 3]);
     }
   }
 }
 
 template <class K, int KK32, int DEPTH, bool RESID, int MG_>
-__device__ __forceinline__ void conv_layer(const char *src, char *dst, const Nbr<K> &nb, bf16x8 (&a)[DEPTH][4],
+__device__ __forceinline__ void conv_layer(const char *src, char *dst, const Nbr<K> &nb, bf16x8 (&a)[DEPTH][MM<K>],
                                            const float *bias, int cg, int lane, const WBuf &wb, uint32_t wl_off,
                                            uint32_t wn_off, int wn_steps) {
   using X = XLive<K, MG_>;
+  constexpr int NM = MM<K>;
   static_assert(KK32 % DEPTH == 0, "ring slot must be a compile-time function of k");
   const int q = lane >> 4, rb = lane_row(lane & 15), qoff = 16 * q;
-  float4 bv[4];  // the epilogue's bias, fetched now (its latency hides under the k-loop)
+  float4 bv[NM];  // the epilogue's bias, fetched now (its latency hides under the k-loop)
 #pragma unroll
-  for (int mm = 0; mm < 4; ++mm) bv[mm] = *(const float4 *)(bias + 64 * cg + 16 * mm + 4 * q);
-  f32x4 acc[4][K::NT][2];
+  for (int mm = 0; mm < NM; ++mm) bv[mm] = *(const float4 *)(bias + 16 * (NM * cg + mm) + 4 * q);
+  f32x4 acc[NM][K::NT][2];
 #pragma unroll
   for (int t = 0; t < K::NT; ++t)
 #pragma unroll
-    for (int mm = 0; mm < 4; ++mm)
+    for (int mm = 0; mm < NM; ++mm)
       if ((X::ZPRE_T >> t) & 1u) acc[mm][t][0] = acc[mm][t][1] = f32x4{};
   int off_cur[K::NT][2], off_nxt[K::NT][2];
   bf16x8 bc[K::NT][2], bn[K::NT][2];
@@ -277,8 +291,10 @@ __device__ __forceinline__ void stem(const char *src, char *dst, const Nbr<K> &n
 template <class K>
 __device__ __forceinline__ void tile(char *smem, const __bf16 *planes, int batch, int board0, int n_blocks,
                                      const bf16x8 *wpk, const float *bias, uint16_t *out) {
-  static_assert(K::EDGE && K::C == 128 && K::CG == 2 && K::MG == 2 && K::WAVES == 4 && !K::ONEBUF,
-                "m16 trunk: C = 128 edge tiles, 2 channel halves x 2 row halves");
+  static_assert(K::EDGE && K::C == 128 && K::WAVES == 4 && !K::ONEBUF &&
+                    ((K::CG == 2 && K::MG == 2) || (K::CG == 4 && K::MG == 1)),
+                "m16 trunk: C = 128 edge tiles, 2 channel halves x 2 row halves (or 4 channel quarters x 1)");
+  constexpr int NM = MM<K>;
   char *X = smem;
   char *Y = smem + K::BUF;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -315,29 +331,29 @@ __device__ __forceinline__ void tile(char *smem, const __bf16 *planes, int batch
   const bf16x8 *wblk = wpk + STEM;
   const float *b = bias + K::C;
   const int cg = wave % K::CG;
-  // per-wave weight streams: layer L, 16-channel tile (4 cg + mm) starts at wblk + L*LAYER + (4 cg + mm)*LSTEPS*64
-  bf16x8 ring[DEPTH][4];
+  // per-wave weight streams: layer L, 16-channel tile (NM cg + mm) starts at wblk + L*LAYER + (NM cg + mm)*LSTEPS*64
+  bf16x8 ring[DEPTH][NM];
   const int n_convs = 2 * n_blocks;
   if (n_convs > 0) {
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d)
 #pragma unroll
-      for (int mm = 0; mm < 4; ++mm) ring[d][mm] = wblk[(size_t)(4 * cg + mm) * LSTEPS * 64 + (size_t)d * 64 + lane];
+      for (int mm = 0; mm < NM; ++mm) ring[d][mm] = wblk[(size_t)(NM * cg + mm) * LSTEPS * 64 + (size_t)d * 64 + lane];
   }
   WBuf wb;
   wb.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)wpk, (short)0, 0x7fffffff, 0x00020000);
   wb.voff = lane * 16;
   const int cg_u = __builtin_amdgcn_readfirstlane(cg);
-  const uint32_t ct0_off = (uint32_t)(STEM + (size_t)(4 * cg_u) * LSTEPS * 64) * 16u;
+  const uint32_t ct0_off = (uint32_t)(STEM + (size_t)(NM * cg_u) * LSTEPS * 64) * 16u;
   for (int L = 0; L < n_convs; ++L) {
     const uint32_t wl_off = ct0_off + (uint32_t)((size_t)L * LAYER * 16u);
     const uint32_t wn_off = (kRingAlways && L + 1 == n_convs) ? wl_off : wl_off + (uint32_t)(LAYER * 16u);
     const int wn_steps = L + 1 < n_convs ? LSTEPS : 0;
     const bool even = (L & 1) == 0;
-    if (wave / K::CG == 0) {
+    if (K::MG == 1 || wave / K::CG == 0) {
       if (even) conv_layer<K, KK32, DEPTH, false, 0>(X, Y, nb, ring, b, cg, lane, wb, wl_off, wn_off, wn_steps);
       else conv_layer<K, KK32, DEPTH, true, 0>(Y, X, nb, ring, b, cg, lane, wb, wl_off, wn_off, wn_steps);
-    } else {
+    } else if constexpr (K::MG == 2) {
       if (even) conv_layer<K, KK32, DEPTH, false, 1>(X, Y, nb, ring, b, cg, lane, wb, wl_off, wn_off, wn_steps);
       else conv_layer<K, KK32, DEPTH, true, 1>(Y, X, nb, ring, b, cg, lane, wb, wl_off, wn_off, wn_steps);
     }
