@@ -1779,6 +1779,14 @@ static int forward_ab(int32_t width, int32_t height, int32_t channels, int32_t n
       default: return 1;
     }
   }
+  // the MFMA-shape clock probe on the C = 256 one-buffer trunk (timing only, wrong results: each 32x32x16 as two
+  // 16x16x32 on the same operands, as code 308 for C = 128) and its reference (2300 = the shipped trunk)
+  if (width == 7 && height == 6 && channels == 256 && cg == 2308)
+    return launch_split<Cfg<256, 256, 7, 6, 4, 4, 8388608, 2, 1, true, true, __bf16, true>, Cfg<256, 128, 7, 6, 4>,
+                        Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+  if (width == 7 && height == 6 && channels == 256 && cg == 2300)
+    return launch_split<Cfg<256, 256, 7, 6, 4, 4, 0, 2, 1, true, true, __bf16, true>, Cfg<256, 128, 7, 6, 4>,
+                        Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
   if (width == 7 && height == 6 && channels == 256 && cg == 254)  // the one-buffer trunk with a 4-deep weight ring
     return launch_split<Cfg<256, 256, 7, 6, 4, 4, 0, 4, 1, true, true, __bf16, true>, Cfg<256, 128, 7, 6, 4>,
                         Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
