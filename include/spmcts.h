@@ -291,8 +291,8 @@ int spmcts_tower_supported(int32_t width, int32_t height, int32_t channels);
 /* The packed weight blob layout the trunk of this shape expects (replaces nothing in the reference: the
  * blob is this library's own format, built by evaluator.HipTowerEvaluator.refresh from the module's
  * state_dict, modules.py:88-107).  SPMCTS_WLAYOUT_32X32: every conv as [Cout/32][taps][Cin/16][64 lanes][8],
- * block and head convs' input channels in the phys_off order.  SPMCTS_WLAYOUT_M16 (the 7x6 C = 128 trunk,
- * tower_m16.h): the stem as 32X32; the block convs as [Cout/16][taps][Cin/32][64 lanes][8] (lane 16q + n:
+ * block and head convs' input channels in the phys_off order.  SPMCTS_WLAYOUT_M16 (the 7x6 C = 128 and
+ * C = 256 trunks, tower_m16.h / tower_wide16.h): the stem as 32X32; the block convs as [Cout/16][taps][Cin/32][64 lanes][8] (lane 16q + n:
  * output channel 16 ct + n, input channels 32 k + 8 q ..) and the block and head convs' input channels in
  * the phys16 order.  Returns -2 for an unsupported shape. */
 #define SPMCTS_WLAYOUT_32X32 0

@@ -994,15 +994,19 @@ __device__ __forceinline__ void head_layer(const char *src, const bf16x8 *w, con
 // One workgroup's tile: boards [board0, board0 + BOARDS) of the batch (board < batch), all layers.
 #include "tower_wide.h"
 #include "tower_m16.h"
+#include "tower_wide16.h"
 
 template <class K>
 __device__ __forceinline__ void tower_tile(char *smem, const __bf16 *planes, int batch, int board0, int n_blocks,
                                            const bf16x8 *wpk, const float *bias, uint16_t *out, uint4 *scr) {
-  if constexpr (K::ONEBUF) {
+  if constexpr (K::ONEBUF && K::M16) {
+    wide16::tile<K>(smem, planes, batch, board0, n_blocks, wpk, bias, out, scr + blockIdx.x * (wide::Scr<K>::PER_WG / 16));
+    return;
+  } else if constexpr (K::ONEBUF) {
     wide::tile<K>(smem, planes, batch, board0, n_blocks, wpk, bias, out, scr + blockIdx.x * (wide::Scr<K>::PER_WG / 16));
     return;
   }
-  if constexpr (K::M16) {
+  if constexpr (K::M16 && !K::ONEBUF) {
     m16::tile<K>(smem, planes, batch, board0, n_blocks, wpk, bias, out);
     return;
   }
@@ -1587,6 +1591,13 @@ static bool wide_tails3() {  // SPMCTS_WIDE_TAILS=3: C = 256 launches with 3-boa
   static const bool v = env_is("SPMCTS_WIDE_TAILS", "3");
   return v;
 }
+// the C = 256 Connect4 trunk on the 16x16x32 one-buffer tiles (tower_wide16.h, its M16 weight layout) unless
+// SPMCTS_TOWER_C256 (=32: round 4's 32x32x16 one-buffer tiles; =3: the 3-board tiles), SPMCTS_WIDE_TAILS or a
+// SPMCTS_TOWER_CG probe code (all on the 32x32x16 layout) selects another set
+static bool c256_m16() {
+  static const bool v = !getenv("SPMCTS_TOWER_C256") && !getenv("SPMCTS_WIDE_TAILS") && !getenv("SPMCTS_TOWER_CG");
+  return v;
+}
 static bool heads_co256() {  // SPMCTS_HEADS_C256=lds: the LDS-staged C = 256 linear heads
   static const bool v = !env_is("SPMCTS_HEADS_C256", "lds");
   return v;
@@ -1609,6 +1620,7 @@ static bool m16_trunk() {
 // A/B library set in the environment is refused (SPMCTS_ERR_AB_SWITCH) rather than silently ignored.
 static constexpr bool m16_trunk() { return true; }
 static constexpr bool c256_board3() { return false; }
+static constexpr bool c256_m16() { return true; }
 static constexpr bool wide_tails3() { return false; }
 static constexpr bool heads_co256() { return true; }
 static constexpr bool heads_co() { return true; }
@@ -1654,12 +1666,16 @@ static int forward_dev(int32_t width, int32_t height, int32_t channels, int32_t 
     if (wide_tails3())  // SPMCTS_WIDE_TAILS=3: the round-3 set, 3-board tail tiles in one kernel with the 6-board body
       return launch_dyn<KW, K3, K3>(planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, pack,
                                     s);
+    if (!c256_m16())  // SPMCTS_TOWER_C256=32: round 4's 32x32x16 one-buffer tiles for every board
+      return launch_dyn<KW, KW, KW>(planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, pack, s);
 #endif
-    // every tile a 6-board one-buffer tile (a batch tail takes one partly empty tile): a kernel that holds the
-    // one-buffer code path only (the set with 3-board tail code inlined beside it spilled twice as much; the
-    // outputs are the same bits either way, test_wide_c256_tiles_bit_identical)
+    // every tile a 6-board one-buffer 16x16x32 tile (tower_wide16.h; a batch tail takes one partly empty tile),
+    // so every board goes through the same arithmetic
     (void)sizeof(K3);
-    return launch_dyn<KW, KW, KW>(planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev, pack, s);
+    (void)sizeof(KW);
+    using KW16 = Cfg<256, 256, 7, 6, 4, 4, 0, 2, 1, true, true, E, true, true>;
+    return launch_dyn<KW16, KW16, KW16>(planes_dev, count_dev, max_batch, n_blocks, weights_dev, bias_dev, features_dev,
+                                        pack, s);
   }
   if (width == 3 && height == 3 && channels == 128)
     return launch_dyn<Cfg<128, 256, 3, 3, 2, 4, 0, 4, 1, false, false, E>, Cfg<128, 192, 3, 3, 2, 4, 0, 4, 1, false, false, E>,
@@ -1689,9 +1705,13 @@ static int forward_host(int32_t width, int32_t height, int32_t channels, int32_t
     using K3 = Cfg<256, 128, 7, 6, 4, 4, 0, 4, 1, false, false, E>;
 #ifdef SPMCTS_AB
     if (c256_board3()) return launch<K3>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+    if (!c256_m16())  // the 32x32x16 one-buffer tiles with 3-board tails (round 4's host path)
+      return launch_split<Cfg<256, 256, 7, 6, 4, 4, 0, 2, 1, true, true, E, true>, K3, K3>(pl, batch, n_blocks,
+                                                                                         weights_dev, bias_dev, ft, s);
 #endif
-    return launch_split<Cfg<256, 256, 7, 6, 4, 4, 0, 2, 1, true, true, E, true>, K3, K3>(pl, batch, n_blocks, weights_dev,
-                                                                                       bias_dev, ft, s);
+    (void)sizeof(K3);
+    return launch<Cfg<256, 256, 7, 6, 4, 4, 0, 2, 1, true, true, E, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev,
+                                                                                 ft, s);
   }
   if (width == 3 && height == 3 && channels == 128)
     return launch<Cfg<128, 256, 3, 3, 2, 4, 0, 4, 1, false, false, E>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
@@ -1939,5 +1959,7 @@ extern "C" int spmcts_tower_supported(int32_t width, int32_t height, int32_t cha
 extern "C" int spmcts_tower_weight_layout(int32_t width, int32_t height, int32_t channels) {
   using namespace tower;
   if (!spmcts_tower_supported(width, height, channels)) return -2;
-  return (width == 7 && height == 6 && channels == 128 && m16_trunk()) ? SPMCTS_WLAYOUT_M16 : SPMCTS_WLAYOUT_32X32;
+  if (width == 7 && height == 6 && channels == 128 && m16_trunk()) return SPMCTS_WLAYOUT_M16;
+  if (width == 7 && height == 6 && channels == 256 && c256_m16()) return SPMCTS_WLAYOUT_M16;
+  return SPMCTS_WLAYOUT_32X32;
 }

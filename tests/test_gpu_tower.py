@@ -66,8 +66,9 @@ def test_tower_matches_fp32_reference(game, blocks, ff, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-def test_tower_rows_independent_of_batch(dtype):
-    net = _net(7, 6, 7, 2, 32)
+@pytest.mark.parametrize("ff", [32, 64])  # C = 128 (tower_m16.h) and C = 256 (tower_wide16.h)
+def test_tower_rows_independent_of_batch(dtype, ff):
+    net = _net(7, 6, 7, 2, ff)
     hip = HipTowerEvaluator(net, dtype=dtype)
     x = _planes(7, 6, 1000, seed=5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     full_p, full_v = hip(x)
@@ -81,12 +82,13 @@ def test_tower_rows_independent_of_batch(dtype):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("n", [1, 37, 700, 1536, 2336, 4000])
-def test_forward_dev_matches_host_count(n, dtype):
+@pytest.mark.parametrize("ff", [32, 64])
+def test_forward_dev_matches_host_count(n, dtype, ff):
     """The device-count launch (row count read on device, full/middle/half workgroups chosen on
     device) gives the host-count results bit for bit on the live rows.  On 256 CUs, 2,336 and 4,000
     rows leave tails of 800 and 928 boards: one round of the 4-board middle tile."""
     W, H, A = 7, 6, 7
-    net = _net(W, H, A, 2, 32)
+    net = _net(W, H, A, 2, ff)
     max_rows = 4096
     x = _planes(W, H, max_rows, seed=5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     hip = HipTowerEvaluator(net, dtype=dtype)
@@ -269,10 +271,14 @@ np.savez(sys.argv[2], **out)
 """
 
 
-def test_wide_c256_tiles_bit_identical(tmp_path):
-    """The one-buffer 6-board C = 256 trunk (tower_wide.h, the product library's default) gives every board
-    the same bits as the 3-board tiles (the A/B library's SPMCTS_TOWER_C256=3, read once per process): host batch (full tiles + tails) and
-    the device-count path on a ragged batch, bf16 and fp16."""
+def test_c256_tile_sets(tmp_path):
+    """The C = 256 trunk's tile sets (each in its own process: the switches are read once):
+    * the A/B library's 6-board one-buffer 32x32x16 tiles (tower_wide.h, round 4's product trunk,
+      SPMCTS_TOWER_C256=32) give every board the same bits as its 3-board tiles (SPMCTS_TOWER_C256=3): host
+      batch (full tiles + tails) and the device-count path on a ragged batch, bf16 and fp16;
+    * the product library's 16x16x32 one-buffer tiles (tower_wide16.h, its own M16 weight blob) agree with
+      them within 1e-2 on probabilities and values (the same products summed in another order; each is
+      checked against the fp32 module by test_tower_matches_fp32_reference)."""
     import os
     import subprocess
     import sys
@@ -281,11 +287,12 @@ def test_wide_c256_tiles_bit_identical(tmp_path):
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     res = {}
-    for tiles in ("3", "6"):
-        # the 3-board tiles are an A/B-library alternate; the 6-board tiles are the product library's trunk
-        env = ab_env(SPMCTS_TOWER_C256="3") if tiles == "3" else product_env()
+    for tiles, env in (("3", ab_env(SPMCTS_TOWER_C256="3")), ("32", ab_env(SPMCTS_TOWER_C256="32")),
+                       ("16", product_env())):
         out = tmp_path / f"c{tiles}.npz"
         subprocess.run([sys.executable, "-c", _WIDE_CHILD, root, str(out)], env=env, check=True, timeout=300)
         res[tiles] = np.load(out)
     for k in res["3"].files:
-        assert np.array_equal(res["3"][k], res["6"][k]), k
+        assert np.array_equal(res["3"][k], res["32"][k]), k
+        assert np.abs(res["16"][k].astype(np.float64) - res["32"][k]).max() < 1e-2, k
+        assert not np.array_equal(res["16"][k], res["32"][k]), k  # the product really runs the other kernel

@@ -141,21 +141,24 @@ def _kernel_handles(path):
 def test_product_library_holds_only_the_shipped_trunk_kernels():
     """The product build (make; no -DSPMCTS_AB) has one trunk kernel set per (board shape, channels,
     dtype): 8 k_tower_dyn (device-count path: 7x6 and 3x3, C = 128 and 256, bf16 and fp16; since round 5
-    the 7x6 C = 256 set is the 6-board one-buffer tiles alone, tails included) and 10 k_tower (host-count
-    path tiles), every Cfg without a
-    timing ablation (ABL = 0), the 7x6 C = 128 trunk only as the 16x16x32 (M16) tiles, the co-resident
-    heads only, and no ring / LDS-heads / ablation kernel."""
+    the 7x6 C = 256 set is the 6-board one-buffer 16x16x32 tiles alone, tails included) and 8 k_tower
+    (host-count path tiles, one per shape and dtype), every Cfg without a timing ablation (ABL = 0), the
+    7x6 C = 128 trunk only as the 16x16x32 (M16) two-buffer tiles and the 7x6 C = 256 trunk only as the M16
+    one-buffer tiles (tower_wide16.h), the co-resident heads only, and no ring / LDS-heads / ablation kernel."""
     path = _lib.LIB_PATH
     if os.path.basename(path) != "libspmcts.so":
         pytest.skip("SPMCTS_LIB points at another build")
     names = _kernel_handles(path)
     dyn = [n for n in names if n.startswith("_ZN5tower11k_tower_dyn")]
     host = [n for n in names if n.startswith("_ZN5tower7k_tower")]
-    assert len(dyn) == 8 and len(host) == 10, (len(dyn), len(host))
+    assert len(dyn) == 8 and len(host) == 8, (len(dyn), len(host))
     # the 7x6 C = 128 kernels: Cfg<128, 256, 7, 6, ..., M16 = true> only (mangled ...Lb0ELb1EE: ONEBUF, M16)
     c128 = [n for n in dyn + host if "CfgILi128ELi256ELi7ELi6E" in n]
     assert len(c128) == 4 and all("Lb0ELb1EE" in n for n in c128), c128
     assert not [n for n in dyn + host if "CfgILi128ELi192ELi7ELi6E" in n or "CfgILi128ELi128ELi7ELi6E" in n]
+    # the 7x6 C = 256 kernels: Cfg<256, 256, 7, 6, ..., ONEBUF = true, M16 = true> only
+    c256 = [n for n in dyn + host if "CfgILi256ELi" in n and "ELi7ELi6E" in n]
+    assert len(c256) == 4 and all("CfgILi256ELi256ELi7ELi6E" in n and "Lb1ELb1EE" in n for n in c256), c256
     # Cfg<C, ROWS, W, H, CG, WAVES, ABL, ...>: the 7th argument is 0 in every instantiation
     cfgs = re.findall(r"(?:CfgI|NS1_I)Li(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E", " ".join(dyn + host))
     assert cfgs and all(c[6] == "0" for c in cfgs)
