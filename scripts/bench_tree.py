@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--blocks-per-tree", type=int, default=0,
                     help="node store per tree (0 = the worst case, no recycling; below it k_compact recycles)")
+    ap.add_argument("--prof", action="store_true",
+                    help="with SPMCTS_LIB=.../libspmcts_prof.so (make prof): shader-clock cycles per sim phase")
     args = ap.parse_args()
     import torch
 
@@ -66,6 +68,15 @@ def main():
 
     for _ in range(args.warmup):
         ply(False)
+    prof = None
+    if args.prof:
+        import ctypes
+
+        prof = ctypes.CDLL(os.environ["SPMCTS_LIB"]).spmcts_ab_tree_prof
+        prof.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+        buf = (ctypes.c_ulonglong * 16)()
+        torch.cuda.synchronize()
+        assert prof(buf, 1) == 0
     c0 = a.counters()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -88,6 +99,15 @@ def main():
                nn_leaves=nn, sims_done=sims, blocks_per_tree=a.blocks_per_tree, ply_ms=wall / args.plies * 1e3,
                compactions=c1["compactions"] - c0["compactions"], blocks_in_use_max=c1["blocks_in_use_max"])
     out["frac_of_8tbs"] = out["achieved_gbs"] / 8000.0
+    if prof is not None:
+        assert prof(buf, 1) == 0
+        names = ("load", "score", "argmax", "leaf", "descend", "rng")
+        for base, kern in ((0, "select"), (8, "expand")):
+            tot = sum(buf[base + i] for i in range(6))
+            out[f"prof_{kern}"] = dict({n: round(buf[base + i] / max(1, tot), 4) for i, n in enumerate(names)},
+                                       phase_cycles=tot, max_launch_cycles=buf[base + 6], max_sims=buf[base + 7])
+        out["prof_cycles_per_sim"] = (sum(buf[i] for i in range(6)) + sum(buf[8 + i] for i in range(6))) / max(1, sims)
+        out["prof_cycles_per_level"] = (sum(buf[i] for i in range(6)) + sum(buf[8 + i] for i in range(6))) / max(1, levels)
     print(json.dumps(out), flush=True)
 
 

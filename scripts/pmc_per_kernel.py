@@ -43,6 +43,16 @@ def main(path, out, pat="."):
         if wc:
             for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
                 row[c.lower()[3:] + "_frac"] = sum(d.get(c, 0.0) for d in ds) / wc
+        # every other counter: its mean per dispatch (and, for SQ_ cycle / wait / active counters, its share
+        # of the waves' cycles)
+        for c in sorted({c for d in ds for c in d if c not in ("ns",)}):
+            if c in ("GRBM_GUI_ACTIVE", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
+                     "SQ_ACTIVE_INST_ANY"):
+                continue
+            tot = sum(d.get(c, 0.0) for d in ds)
+            row[c.lower() + "_per_dispatch"] = tot / len(ds)
+            if wc and c.startswith("SQ_") and c != "SQ_WAVE_CYCLES" and ("CYCLES" in c or "WAIT" in c or "ACTIVE" in c):
+                row[c.lower()[3:] + "_frac"] = tot / wc
         res[k] = row
     json.dump(res, open(out, "w"), indent=1)
     for k, v in res.items():

@@ -339,6 +339,13 @@ __device__ __forceinline__ void reset_tree(const View &v, int tree, int player, 
 }
 
 // terminal value of _expand_node (mcts.py:305-313) for `tree`'s own strong_play; r = reward * mover
+__device__ __forceinline__ double terminal_value(bool strong, Board parent, int r) {
+  if (strong) {
+    const int num_steps = popc(parent.pos | parent.neg) + 1;  // np.sum(np.abs(state)) + 1
+    return (1.18 - ((double)(9 * num_steps) / 350.0)) * (double)r;
+  }
+  return (double)r;
+}
 __device__ __forceinline__ double terminal_value(const View &v, int tree, Board parent, int r) {
   if (v.tstrong[tree]) {
     const int num_steps = popc(parent.pos | parent.neg) + 1;  // np.sum(np.abs(state)) + 1
@@ -550,23 +557,74 @@ __global__ __launch_bounds__(256) void k_compact(View v, int n_active) {
 // ----------------------------------------------------------------------------
 // kernel: select (search_node, mcts.py:340-367)
 // ----------------------------------------------------------------------------
+// P-lane group reductions on DPP lane permutations (a few cycles each) instead of ds_bpermute (an LDS
+// round trip each, ~100 cycles on the tree kernels' dependent chain): partners lane ^ 1 and lane ^ 2
+// (quad_perm), then lane ^ 7 (row_half_mirror: the other quad of the 8-lane group) and lane ^ 15
+// (row_mirror: the other half of a 16-lane group).  After the two quad steps every lane holds its quad's
+// result, so the mirror steps combine whole quads / halves: every lane ends with the group's result.
+// Only lanes of the same group are read (the permutations stay within 4, 8 or 16 lanes).
+enum { DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140 };
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int x) {
+  return __builtin_amdgcn_mov_dpp(x, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double x) {
+  const int2 v = __builtin_bit_cast(int2, x);
+  return __builtin_bit_cast(double, make_int2(dpp_i<CTRL>(v.x), dpp_i<CTRL>(v.y)));
+}
+
+// argmax with the lowest index on ties (associative and commutative, so the butterfly order does not
+// change the result)
+template <int P, int CTRL>
+__device__ __forceinline__ void argmax_step(double &s, int &idx) {
+  const double so = dpp_d<CTRL>(s);
+  const int io = dpp_i<CTRL>(idx);
+  if (so > s || (so == s && io < idx)) {
+    s = so;
+    idx = io;
+  }
+}
 template <int P>
 __device__ __forceinline__ void group_argmax(double &s, int &idx) {
-#pragma unroll
-  for (int off = P / 2; off > 0; off >>= 1) {
-    const double so = __shfl_xor(s, off, P);
-    const int io = __shfl_xor(idx, off, P);
-    if (so > s || (so == s && io < idx)) {
-      s = so;
-      idx = io;
-    }
+  static_assert(P == 8 || P == 16, "tree groups of 8 or 16 lanes");
+  argmax_step<P, DPP_XOR1>(s, idx);
+  argmax_step<P, DPP_XOR2>(s, idx);
+  argmax_step<P, DPP_HALF_MIRROR>(s, idx);
+  if constexpr (P == 16) argmax_step<P, DPP_MIRROR>(s, idx);
+}
+
+// group_argmax that also hands every lane the winning lane's child fields (the payload moves with the
+// index through the butterfly, so no ds_bpermute from lane `a` afterwards)
+template <int CTRL>
+__device__ __forceinline__ void argmax_carry_step(double &s, int &idx, int &c0, int &c1, int &c2, double &d0) {
+  const double so = dpp_d<CTRL>(s), d0o = dpp_d<CTRL>(d0);
+  const int io = dpp_i<CTRL>(idx), c0o = dpp_i<CTRL>(c0), c1o = dpp_i<CTRL>(c1), c2o = dpp_i<CTRL>(c2);
+  if (so > s || (so == s && io < idx)) {
+    s = so;
+    idx = io;
+    c0 = c0o;
+    c1 = c1o;
+    c2 = c2o;
+    d0 = d0o;
   }
+}
+template <int P>
+__device__ __forceinline__ void group_argmax_carry(double &s, int &idx, int &c0, int &c1, int &c2, double &d0) {
+  static_assert(P == 8 || P == 16, "tree groups of 8 or 16 lanes");
+  argmax_carry_step<DPP_XOR1>(s, idx, c0, c1, c2, d0);
+  argmax_carry_step<DPP_XOR2>(s, idx, c0, c1, c2, d0);
+  argmax_carry_step<DPP_HALF_MIRROR>(s, idx, c0, c1, c2, d0);
+  if constexpr (P == 16) argmax_carry_step<DPP_MIRROR>(s, idx, c0, c1, c2, d0);
 }
 
 template <int P>
 __device__ __forceinline__ int group_or(int x) {
-#pragma unroll
-  for (int off = P / 2; off > 0; off >>= 1) x |= __shfl_xor(x, off, P);
+  static_assert(P == 8 || P == 16, "tree groups of 8 or 16 lanes");
+  x |= dpp_i<DPP_XOR1>(x);
+  x |= dpp_i<DPP_XOR2>(x);
+  x |= dpp_i<DPP_HALF_MIRROR>(x);
+  if constexpr (P == 16) x |= dpp_i<DPP_MIRROR>(x);
   return x;
 }
 
@@ -741,6 +799,7 @@ enum { SIM_DONE = 0, SIM_PENDING = 1, SIM_LEAK = 2, SIM_ERROR = -1 };
 // scores.  Every store a sim or backup makes to these nodes is made to the registers as well (the
 // same arithmetic), so depth 0 reads no memory.
 struct TreeRoot {
+  bool strong;  // the tree's strong_play (read once: a global load in a sim would wait on its stores)
   int node, cb, player, n, vl;
   double w;  // the root's w (terminal backups write it from here, no read-modify-write)
   Board b;
@@ -755,6 +814,7 @@ __device__ __forceinline__ TreeRoot load_root(const View &v, int tree) {
   constexpr int P = G::APAD;
   const size_t nb = nbase<G>(v, tree);
   TreeRoot R;
+  R.strong = v.tstrong[tree] != 0;
   R.node = v.root[tree];
   R.b = Board{v.rpos[tree], v.rneg[tree]};
   R.player = v.rplayer[tree];
@@ -784,17 +844,135 @@ __device__ __forceinline__ TreeRoot load_root(const View &v, int tree) {
 }
 
 // The path of the sim in flight, in LDS (one group per tree): node ids and, per level, the node's n, vl
-// (this sim's virtual loss included) and w as this sim read them.  One wave owns the tree, so nothing changes
-// them between the read and this sim's backup: a terminal backup writes n + 1, w + value, vl - 1 from here
-// instead of reading the nodes again (one memory round trip less per terminal sim).
+// (this sim's virtual loss included) and w as this sim read them, and where the node's record sits (cs: a
+// BlockCache slot, kRootRegs for the root and the root's children, kUncached).  One wave owns the tree, so
+// nothing changes them between the read and this sim's backup: a terminal backup writes n + 1, w + value,
+// vl - 1 from here instead of reading the nodes again (one memory round trip less per terminal sim).
 struct PathLds {
-  int32_t *node, *n, *vl;
+  int32_t *node, *n, *vl, *cs;
   double *w;
 };
+enum { kUncached = -1, kRootRegs = -2 };
+
+// Per-launch LDS copies of the child blocks a tree's sims read (round 5).  One wave owns a tree for the
+// whole launch, so a block's record, copied in from global memory the first time a level reads it, stays
+// exact as long as every store the launch makes to the block is made to the copy as well (write-through:
+// the global record stays current for later launches).  A level that hits reads LDS instead of issuing a
+// dependent global load, and a sim whose stores all went to copied blocks or to the root and its children
+// (kept in registers for the launch, TreeRoot) needs no fence before the next sim: nothing it wrote is read
+// back from global memory in this launch.  With the copies full, stores to uncopied blocks set `dirty`,
+// and the next global read of node records waits on a workgroup fence first (round 4's per-sim fence).
+// The copies hold everything a level reads (n, vl, child block, p, w, the valid mask); the strong-play
+// flag is written to global memory only (nothing in a launch reads it).
+template <int P, int S>
+struct BlockCache {
+  static constexpr int BYTES = NodeRec<P>::BYTES;
+  int32_t *tag;  // [S] tree-local block index of each copy (16-byte aligned)
+  char *rec;     // [S][BYTES] the copies
+  int cnt = 0;   // copies in use (group-uniform)
+  bool dirty = false;  // stores to uncopied blocks since the last fence (group-uniform)
+  __device__ __forceinline__ void fence_if_dirty() {
+    if (dirty) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      dirty = false;
+    }
+  }
+  // the slot holding block `blk` or kUncached; every lane may ask for its own block
+  __device__ __forceinline__ int find(int blk) const {
+    int hit = kUncached;
+    if constexpr (S > 0) {
+#pragma unroll
+      for (int i = 0; i < S / 4; ++i) {
+        if (4 * i >= cnt) break;
+        const int4 t = ((const int4 *)tag)[i];
+        if (t.x == blk && 4 * i + 0 < cnt) hit = 4 * i + 0;
+        if (t.y == blk && 4 * i + 1 < cnt) hit = 4 * i + 1;
+        if (t.z == blk && 4 * i + 2 < cnt) hit = 4 * i + 2;
+        if (t.w == blk && 4 * i + 3 < cnt) hit = 4 * i + 3;
+      }
+    }
+    return hit;
+  }
+  // copy block `blk` (global record `g`) into a free slot (group-uniform call); kUncached when full
+  __device__ __forceinline__ int insert(int blk, const char *g, int lane) {
+    if constexpr (S == 0) {
+      return kUncached;
+    } else {
+      if (cnt >= S) return kUncached;
+      fence_if_dirty();
+      const int s = cnt++;
+      const uint4 *src = (const uint4 *)(g + 32 * lane);  // P lanes x 32 bytes = the record
+      const uint4 a = src[0], b = src[1];
+      uint4 *dst = (uint4 *)(rec + s * BYTES + 32 * lane);
+      dst[0] = a;
+      dst[1] = b;
+      if (lane == 0) tag[s] = blk;
+      return s;
+    }
+  }
+  // a new block's copy from the values the caller stores to global memory (k_expand_vl); kUncached when full
+  __device__ __forceinline__ int insert_new(int blk, int lane, float p, uint32_t vm) {
+    if constexpr (S == 0) {
+      return kUncached;
+    } else {
+      if (cnt >= S) return kUncached;
+      const int s = cnt++;
+      char *r = rec + s * BYTES;
+      ((int32_t *)(r + NodeRec<P>::N))[lane] = 0;
+      ((int32_t *)(r + NodeRec<P>::VL))[lane] = 0;
+      ((int32_t *)(r + NodeRec<P>::C))[lane] = -1;
+      ((float *)(r + NodeRec<P>::PR))[lane] = p;
+      ((double *)(r + NodeRec<P>::W))[lane] = 0.0;
+      if (lane == 0) {
+        *(uint32_t *)(r + NodeRec<P>::VM) = vm;
+        tag[s] = blk;
+      }
+      return s;
+    }
+  }
+  template <class T>
+  __device__ __forceinline__ T &at(int s, int off, int a) const {
+    return ((T *)(rec + s * BYTES + off))[a];
+  }
+  __device__ __forceinline__ uint32_t vm(int s) const { return *(const uint32_t *)(rec + s * BYTES + NodeRec<P>::VM); }
+};
+
+#ifdef SPMCTS_TREE_PROF
+// Profiling build only (make prof: libspmcts_prof.so): shader-clock cycles per sim phase, summed over the
+// trees, per kernel (select: [0, 8), expand: [8, 16)) -- [0..5] the phases of TP_* below, [6] the largest
+// per-tree launch time, [7] the most sims one tree ran in one launch
+__device__ unsigned long long g_tprof[16];
+enum { TP_LOAD = 0, TP_SCORE = 1, TP_ARGMAX = 2, TP_LEAF = 3, TP_DESCEND = 4, TP_RNG = 5, TP_OTHER = 5 };
+#define TP_MARK(sc, i)                                 \
+  do {                                                 \
+    const unsigned long long t_ = clock64();           \
+    (sc).tp[i] += t_ - (sc).tlast;                     \
+    (sc).tlast = t_;                                   \
+  } while (0)
+#else
+#define TP_MARK(sc, i) \
+  do {                 \
+  } while (0)
+#endif
+
 // The tree's counters of one kernel launch (the same value in every lane of the group), added to the
 // arena's counters once at the end of the launch instead of a read-modify-write per sim.
 struct SimCnt {
   int64_t sims = 0, depth = 0, term = 0, leak = 0, nn = 0, hwm = 0;
+#ifdef SPMCTS_TREE_PROF
+  unsigned long long tp[6] = {0, 0, 0, 0, 0, 0}, tlast = 0, t0 = 0;
+  int64_t sims0 = 0;
+  __device__ void prof_begin() {
+    t0 = tlast = clock64();
+    sims0 = sims;
+  }
+  __device__ void prof_flush(int base) const {
+    const unsigned long long t1 = clock64();
+    for (int i = 0; i < 6; ++i) atomicAdd(&g_tprof[base + i], tp[i]);
+    atomicMax(&g_tprof[base + 6], t1 - t0);
+    atomicMax(&g_tprof[base + 7], (unsigned long long)(sims - sims0));
+  }
+#endif
   __device__ void flush(int64_t *cnt) const {
     cnt[C_SIMS] += sims;
     cnt[C_DEPTH] += depth;
@@ -804,21 +982,17 @@ struct SimCnt {
     cnt[C_HWM] = max(cnt[C_HWM], hwm);
   }
 };
-// sim_vl's result for a terminal leaf among the root's children: the sim read no memory (depth 0 scores
-// from registers) and wrote only the root's record and its child's, which no later sim of this launch
-// reads from memory before the fill's closing fence -- so the next sim needs no fence first.
-enum { SIM_DONE_ROOT = 3 };
 
 // One search_node with virtual loss (mcts.py:340-367) for pending slot j of `tree`, run by the
 // tree's P-lane group.  vl += 1 on every node passed (mcts.py:345), children scored with
 // q = (w - vl)/(n + vl) and u = c p sqrt(N + vl_parent)/(1 + n + vl) (mcts.py:59-78), pending leaves
 // locked (child-block index -2, score -1e10, mcts.py:86-88).  Returns SIM_PENDING with the leaf
-// locked and its path stashed in slot j, SIM_DONE (SIM_DONE_ROOT at depth 0) for a terminal leaf (backed
-// up, path vl removed), SIM_LEAK for a leak, SIM_ERROR on a corrupt tree; R (the root in registers) is
+// locked and its path stashed in slot j, SIM_DONE for a terminal leaf (backed up, path vl removed),
+// SIM_LEAK for a leak, SIM_ERROR on a corrupt tree; R (the root in registers) and the block copies bc are
 // updated to match.  The return value is uniform across the group.
-template <class G>
+template <class G, int S>
 __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng, bool &terr, const PathLds &pl,
-                      bool noise, double nz, SimCnt &sc) {
+                      bool noise, double nz, SimCnt &sc, BlockCache<G::APAD, S> &bc) {
   constexpr int P = G::APAD;
   const int lane = threadIdx.x & (P - 1);
   const int gbase = (threadIdx.x & 63) & ~(P - 1);
@@ -832,6 +1006,7 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
   int node_vl = R.vl + 1;  // this sim's virtual loss on the node (mcts.py:345)
   double node_w = R.w;
   int cb = R.cb;
+  int ncs = kRootRegs;  // where path node `depth`'s record sits
   R.vl += 1;
   int depth = 0;
   int a0 = 0;  // the root child this sim took (path node 1)
@@ -841,8 +1016,12 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
       pl.n[depth] = node_n;
       pl.vl[depth] = node_vl;
       pl.w[depth] = node_w;
-      nd_vl<P>(v, nb + node) = node_vl;
+      pl.cs[depth] = ncs;
+      if (ncs >= 0) bc.template at<int32_t>(ncs, NodeRec<P>::VL, node % P) = node_vl;
     }
+    // the global store of the path's virtual loss waits for the sim's end (one store per path node, all
+    // at once): gfx950's vmcnt counts stores too, so a store here would hold up the next level's loads
+    if (ncs == kUncached) bc.dirty = true;
     if (depth == 1 && lane == a0) R.cvl = node_vl;  // the root child's vl, in registers too
     if (cb < 0) {
       if (lane == 0) set_err(v, SPMCTS_ERR_STATE);
@@ -852,6 +1031,7 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
     int cn = 0, cc = -1, cvl = 0;
     double cw = 0.0;
     float cp = 0.f;
+    int lcs = kRootRegs;  // where this level's child block (cb) sits
     if (depth == 0) {  // the root's child block, from registers
       vm = R.vm;
       cn = R.cn;
@@ -860,21 +1040,44 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
       cc = R.cc;
       cvl = R.cvl;
     } else {
-      vm = nd_vm<P>(v, bb + cb);
-      const size_t ci = nb + (size_t)cb * P + lane;
-      if (lane < G::A) {
-        cn = nd_n<P>(v, ci);
-        cw = nd_w<P>(v, ci);
-        cp = nd_p<P>(v, ci);
-        cc = nd_c<P>(v, ci);
-        cvl = nd_vl<P>(v, ci);
+      lcs = bc.find(cb);
+      if (lcs == kUncached) lcs = bc.insert(cb, nd_rec<P>(v, nb + (size_t)cb * P), lane);
+      if (lcs >= 0) {
+        vm = bc.vm(lcs);
+        if (lane < G::A) {
+          cn = bc.template at<int32_t>(lcs, NodeRec<P>::N, lane);
+          cw = bc.template at<double>(lcs, NodeRec<P>::W, lane);
+          cp = bc.template at<float>(lcs, NodeRec<P>::PR, lane);
+          cc = bc.template at<int32_t>(lcs, NodeRec<P>::C, lane);
+          cvl = bc.template at<int32_t>(lcs, NodeRec<P>::VL, lane);
+        }
+      } else {
+        bc.fence_if_dirty();
+        vm = nd_vm<P>(v, bb + cb);
+        const size_t ci = nb + (size_t)cb * P + lane;
+        if (lane < G::A) {
+          cn = nd_n<P>(v, ci);
+          cw = nd_w<P>(v, ci);
+          cp = nd_p<P>(v, ci);
+          cc = nd_c<P>(v, ci);
+          cvl = nd_vl<P>(v, ci);
+        }
       }
     }
+#ifdef SPMCTS_TREE_PROF
+    // (profiling: the loads completed before the jitter, to time the two apart)
+    if (cn == -12345 || cw == -1.5 || cp == -1.5f || cvl == -12345 || vm == 0xdeadbeefu) sc.tp[TP_OTHER] += 1;
+    TP_MARK(sc, TP_LOAD);
+#endif
     // the jitter does not depend on the child block: drawn here, it overlaps the loads above
     bool terr_j = false;
     const double jit = rng_group<G>(v, rng, lane, gbase, &terr_j);
     // valid (mcts.py:86-88): valid move and not locked by a pending sim
     const bool valid = (lane < G::A) && ((vm >> lane) & 1u) && cc != -2;
+#ifdef SPMCTS_TREE_PROF
+    if (jit == -1.5) sc.tp[TP_OTHER] += 1;
+    TP_MARK(sc, TP_RNG);
+#endif
     double score = -10000000000.0;
     if (valid) {
       // q (mcts.py:59-62): (w - vl) / (n + vl)
@@ -886,6 +1089,7 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
       score = (player > 0 ? q : -q) + u;
     }
     if (!group_or<P>(valid ? 1 : 0)) {  // mcts.py:349-354: return, virtual loss left in place
+      for (int k = lane; k <= depth; k += P) nd_vl<P>(v, nb + pl.node[k]) = pl.vl[k];
       sc.leak += 1;
       return SIM_LEAK;
     }
@@ -893,13 +1097,13 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
     double s = -INFINITY;
     if (lane < G::A) s = score + 0.000001 * jit;
     rng_advance(v, rng, G::A);
+    TP_MARK(sc, TP_SCORE);
     int a = lane;
-    group_argmax<P>(s, a);
-    const int cc_a = __shfl(cc, gbase + a, 64);
-    const int cn_a = __shfl(cn, gbase + a, 64);
-    const int cvl_a = __shfl(cvl, gbase + a, 64);
-    const double cw_a = __shfl(cw, gbase + a, 64);
+    int cc_a = cc, cn_a = cn, cvl_a = cvl;
+    double cw_a = cw;
+    group_argmax_carry<P>(s, a, cc_a, cn_a, cvl_a, cw_a);  // lane a's child fields in every lane
     const int child = cb * P + a;
+    TP_MARK(sc, TP_ARGMAX);
     if (cc_a < 0) {
       // leaf: _expand_node (mcts.py:301-321)
       Board nb2 = b;
@@ -908,20 +1112,35 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
       if (done) {
         // terminal: backup (mcts.py:94-98) then remove the path's virtual loss (:365); one lane per
         // path node, the values this sim read (pl: written by lane 0 of this wave, LDS stays in order)
-        const double val = terminal_value(v, tree, b, rew * player);
-        const bool strong = v.tstrong[tree] != 0;
+        const double val = terminal_value(R.strong, b, rew * player);
+        const bool strong = R.strong;
+        int unc = 0;
         for (int k = lane; k <= depth; k += P) {
-          const size_t idx = nb + pl.node[k];
-          nd_n<P>(v, idx) = pl.n[k] + 1;
-          nd_w<P>(v, idx) = pl.w[k] + val;
+          const int nk = pl.node[k], ck = pl.cs[k];
+          const size_t idx = nb + nk;
+          const int32_t n1 = pl.n[k] + 1, vl1 = pl.vl[k] - 1;
+          const double w1 = pl.w[k] + val;
+          nd_n<P>(v, idx) = n1;
+          nd_w<P>(v, idx) = w1;
           if (strong) nd_f<P>(v, idx) = 1;
-          nd_vl<P>(v, idx) = pl.vl[k] - 1;
+          nd_vl<P>(v, idx) = vl1;
+          if (ck >= 0) {
+            bc.template at<int32_t>(ck, NodeRec<P>::N, nk % P) = n1;
+            bc.template at<double>(ck, NodeRec<P>::W, nk % P) = w1;
+            bc.template at<int32_t>(ck, NodeRec<P>::VL, nk % P) = vl1;
+          }
+          unc |= ck == kUncached;
         }
         if (lane == 0) {
           nd_n<P>(v, nb + child) = cn_a + 1;
           nd_w<P>(v, nb + child) = cw_a + val;
           if (strong) nd_f<P>(v, nb + child) = 1;
+          if (lcs >= 0) {
+            bc.template at<int32_t>(lcs, NodeRec<P>::N, a) = cn_a + 1;
+            bc.template at<double>(lcs, NodeRec<P>::W, a) = cw_a + val;
+          }
         }
+        if (group_or<P>(unc) || lcs == kUncached) bc.dirty = true;
         R.n += 1;  // the root is path node 0
         R.vl -= 1;
         R.w += val;
@@ -937,7 +1156,11 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
         sc.term += 1;
       } else {
         const size_t pb = (size_t)ps * G::MAXD;
-        for (int k = lane; k <= depth; k += P) v.pnode[pb + k] = pl.node[k];
+        for (int k = lane; k <= depth; k += P) {
+          const int nk = pl.node[k];
+          v.pnode[pb + k] = nk;
+          nd_vl<P>(v, nb + nk) = pl.vl[k];
+        }
       }
       sc.sims += 1;
       sc.depth += depth + 1;
@@ -946,6 +1169,7 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
         if (!done) {
           // lock the leaf (mcts.py:359); the path was stashed above for the backup
           nd_c<P>(v, nb + child) = -2;
+          if (lcs >= 0) bc.template at<int32_t>(lcs, NodeRec<P>::C, a) = -2;
           v.plen[ps] = depth + 1;
           v.leaf[ps] = child;
           v.lpos[ps] = nb2.pos;
@@ -954,8 +1178,10 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
           v.need[ps] = 1;
         }
       }
+      if (!done && lcs == kUncached) bc.dirty = true;
       if (!done && depth == 0 && lane == a) R.cc = -2;
-      return done ? (depth == 0 ? SIM_DONE_ROOT : SIM_DONE) : SIM_PENDING;
+      TP_MARK(sc, TP_LEAF);
+      return done ? SIM_DONE : SIM_PENDING;
     }
     if (depth == 0) a0 = a;
     play<G>(b, a, player);
@@ -964,8 +1190,10 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
     node_vl = cvl_a + 1;
     node_w = cw_a;
     cb = cc_a;
+    ncs = lcs;  // the child's record is in this level's block
     player = -player;
     ++depth;
+    TP_MARK(sc, TP_DESCEND);
     if (depth >= G::MAXD) {
       if (lane == 0) set_err(v, SPMCTS_ERR_STATE);
       return SIM_ERROR;
@@ -974,38 +1202,45 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
 }
 
 // Refill pending slot j: start sims until one waits for the network or the tree's budget of
-// search_node calls is spent (`started` counts them, mcts.py:328-331 submits `iterations`).
-template <class G>
+// search_node calls is spent (`started` counts them, mcts.py:328-331 submits `iterations`).  No fence
+// between sims: a sim reads what the previous one wrote from the block copies or the registers, and
+// the copies' `dirty` rule fences before any global read of node records after an uncopied store.
+template <class G, int S>
 __device__ int fill_slot_vl(const View &v, int tree, int j, int limit, int &started, TreeRoot &R, TreeRng &rng,
-                            bool &terr, const PathLds &pl, bool noise, double nz, SimCnt &sc) {
-  bool unfenced = false;
+                            bool &terr, const PathLds &pl, bool noise, double nz, SimCnt &sc,
+                            BlockCache<G::APAD, S> &bc) {
   while (started < limit) {
     ++started;
-    const int r = sim_vl<G>(v, tree, j, R, rng, terr, pl, noise, nz, sc);
-    if (r == SIM_DONE_ROOT) {  // read nothing, wrote the root and a root child: no fence needed yet
-      unfenced = true;
-      continue;
-    }
-    // the next sim reads what this one wrote (lane 0's stores, other lanes' loads): one wave owns
-    // the tree, so a workgroup-scope fence (stores complete, same CU's L1) is enough
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    unfenced = false;
+    const int r = sim_vl<G, S>(v, tree, j, R, rng, terr, pl, noise, nz, sc, bc);
     if (r == SIM_PENDING || r == SIM_ERROR) return r;
   }
-  if (unfenced) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // before the next backup's reads
   return SIM_DONE;
 }
 
+// LDS block copies per tree: none in the shipped kernels.  Measured (profiles/r05/tree2/): with 16
+// copies per tree the isolated expand ran 250 -> 295-300 us and select unchanged (a launch starts with no
+// copies, so most blocks are copied once and read once; and the levels of a sim are a chain of short
+// dependent LDS / permute / FP64 latencies, not memory round trips: scripts/bench_tree.py --prof).
+// The A/B library keeps them behind SPMCTS_TREE_COPIES=1.
+template <int TB>
+constexpr int kCopies = 0;
+
 // First step of a search: fill the K slots of every searching tree.
-template <class G, int TB = 64>
+template <class G, int TB = 64, int S = kCopies<TB>>
 __global__ __launch_bounds__(TB) void k_select_vl(View v, int n_active) {
   constexpr int P = G::APAD;
   constexpr int GPB = TB / P;
-  __shared__ int32_t s_node[GPB][G::MAXD], s_n[GPB][G::MAXD], s_vl[GPB][G::MAXD];
+  constexpr int S1 = S > 0 ? S : 4;
+  __shared__ int32_t s_node[GPB][G::MAXD], s_n[GPB][G::MAXD], s_vl[GPB][G::MAXD], s_cs[GPB][G::MAXD];
   __shared__ double s_w[GPB][G::MAXD];
+  __shared__ __attribute__((aligned(16))) int32_t s_tag[GPB][S1];
+  __shared__ __attribute__((aligned(16))) char s_rec[S > 0 ? GPB : 1][S > 0 ? S : 1][NodeRec<P>::BYTES];
   const int lane = threadIdx.x & (P - 1);
   const int grp = threadIdx.x / P;
-  const PathLds pl{s_node[grp], s_n[grp], s_vl[grp], s_w[grp]};
+  const PathLds pl{s_node[grp], s_n[grp], s_vl[grp], s_cs[grp], s_w[grp]};
+  BlockCache<P, S> bc;
+  bc.tag = s_tag[grp];
+  bc.rec = S > 0 ? &s_rec[grp][0][0] : nullptr;
   const int slot = blockIdx.x * (int)(blockDim.x / P) + grp;  // blockDim = 64 (GPB trees) or P (one tree)
   if (slot >= n_active) return;
   const int tree = v.active[slot];
@@ -1020,12 +1255,18 @@ __global__ __launch_bounds__(TB) void k_select_vl(View v, int n_active) {
   TreeRoot R = load_root<G>(v, tree);
   bool terr = false;
   SimCnt sc;
+#ifdef SPMCTS_TREE_PROF
+  sc.prof_begin();
+#endif
   const int kt = v.tK[tree];  // this tree's sims in flight (its own thread_count, <= K)
   for (int j = 0; j < kt; ++j) {
     if (v.need[tree * v.K + j]) continue;
-    if (fill_slot_vl<G>(v, tree, j, limit, started, R, rng, terr, pl, noise, nz, sc) == SIM_ERROR) return;
+    if (fill_slot_vl<G, S>(v, tree, j, limit, started, R, rng, terr, pl, noise, nz, sc, bc) == SIM_ERROR) return;
   }
   if (lane == 0) {
+#ifdef SPMCTS_TREE_PROF
+    sc.prof_flush(0);
+#endif
     sc.flush(v.cnt + (size_t)tree * C_NCNT);
     v.tstarted[tree] = started;
     if (terr) set_err(v, SPMCTS_ERR_TAPE);
@@ -1302,14 +1543,14 @@ __global__ __launch_bounds__(64) void k_expand(View v, const float *probs0, cons
 // earlier slots of the same tree have changed the shared ancestors.  Pending leaves of trees that
 // are not searching (a _set_node expansion, slot 0, path length 0) are completed without a refill.
 // ----------------------------------------------------------------------------
-template <class G, int TB>
+template <class G, int TB, int S>
 __device__ __forceinline__ void expand_vl_body(View v, const float *probs0, const float *values0,
                                                const float *probs1, const float *values1);
 
-template <class G, int TB = 64>
+template <class G, int TB = 64, int S = kCopies<TB>>
 __global__ __launch_bounds__(TB) void k_expand_vl(View v, const float *probs0, const float *values0,
                                                   const float *probs1, const float *values1) {
-  expand_vl_body<G, TB>(v, probs0, values0, probs1, values1);
+  expand_vl_body<G, TB, S>(v, probs0, values0, probs1, values1);
 }
 
 // The same held to 96 registers (SPMCTS_EXPAND_CO=1, a timing variant): its waves then fit on a SIMD
@@ -1318,17 +1559,20 @@ __global__ __launch_bounds__(TB) void k_expand_vl(View v, const float *probs0, c
 template <class G>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_expand_vl_co(
     View v, const float *probs0, const float *values0, const float *probs1, const float *values1) {
-  expand_vl_body<G, 64>(v, probs0, values0, probs1, values1);
+  expand_vl_body<G, 64, 0>(v, probs0, values0, probs1, values1);
 }
 
-template <class G, int TB>
+template <class G, int TB, int S>
 __device__ __forceinline__ void expand_vl_body(View v, const float *probs0, const float *values0,
                                                const float *probs1, const float *values1) {
   constexpr int P = G::APAD;
   constexpr int GPB = TB / P;
   constexpr int KMAX = P;  // slots whose records one lane each prefetches (spmcts_arena_create: K <= P)
-  __shared__ int32_t s_node[GPB][G::MAXD], s_n[GPB][G::MAXD], s_vl[GPB][G::MAXD];
+  constexpr int S1 = S > 0 ? S : 4;
+  __shared__ int32_t s_node[GPB][G::MAXD], s_n[GPB][G::MAXD], s_vl[GPB][G::MAXD], s_cs[GPB][G::MAXD];
   __shared__ double s_w[GPB][G::MAXD];
+  __shared__ __attribute__((aligned(16))) int32_t s_tag[GPB][S1];
+  __shared__ __attribute__((aligned(16))) char s_rec[S > 0 ? GPB : 1][S > 0 ? S : 1][NodeRec<P>::BYTES];
   // the prefetched path nodes (k < P) and network outputs of each slot, per tree group; each LDS word
   // is written and later read by the same wave (LDS operations of a wave stay in order)
   __shared__ int32_t s_pnode[GPB][KMAX][P];
@@ -1339,7 +1583,10 @@ __device__ __forceinline__ void expand_vl_body(View v, const float *probs0, cons
   const int gbase = (threadIdx.x & 63) & ~(P - 1);
   const int tree = (blockIdx.x * blockDim.x + threadIdx.x) / P;
   if (tree >= v.T) return;
-  const PathLds pl{s_node[grp], s_n[grp], s_vl[grp], s_w[grp]};
+  const PathLds pl{s_node[grp], s_n[grp], s_vl[grp], s_cs[grp], s_w[grp]};
+  BlockCache<P, S> bc;
+  bc.tag = s_tag[grp];
+  bc.rec = S > 0 ? &s_rec[grp][0][0] : nullptr;
   const int K = v.K;
   const size_t nb = nbase<G>(v, tree);
   const size_t bb = (size_t)tree * v.cap;
@@ -1394,6 +1641,9 @@ __device__ __forceinline__ void expand_vl_body(View v, const float *probs0, cons
   }
   bool terr = false;
   SimCnt sc;
+#ifdef SPMCTS_TREE_PROF
+  sc.prof_begin();
+#endif
   // one copy of the slot body (a rolled loop: the unrolled form was 70 KB of code, more than the
   // instruction cache two CUs share, for a kernel that runs one wave per CU on a latency chain)
 #pragma unroll 1
@@ -1409,28 +1659,112 @@ __device__ __forceinline__ void expand_vl_body(View v, const float *probs0, cons
         return;
       }
       ++used;
+      const float pnew = lane < G::A ? s_pr[grp][j][lane] : 0.f;
+      const uint32_t vmnew = legal_mask<G>(Board{lpos, lneg});
       {
         const size_t ci = nb + (size_t)blk * P + lane;
         nd_n<P>(v, ci) = 0;
         nd_w<P>(v, ci) = 0.0;
-        nd_p<P>(v, ci) = lane < G::A ? s_pr[grp][j][lane] : 0.f;
+        nd_p<P>(v, ci) = pnew;
         nd_c<P>(v, ci) = -1;
         nd_f<P>(v, ci) = 0;
         nd_vl<P>(v, ci) = 0;
       }
       const double val = (double)s_vr[grp][j] * (double)mover;
-      // backup of the path (distinct nodes): one lane per path node, the node ids prefetched
-      for (int k = lane; k < plen; k += P) {
-        const size_t idx = nb + (k < P ? s_pnode[grp][j][k] : v.pnode[(size_t)ps * G::MAXD + k]);
-        nd_n<P>(v, idx) += 1;
-        nd_w<P>(v, idx) += val;
-        nd_vl<P>(v, idx) -= 1;
+      if (!refill) {
+        // no sims in this launch (nothing copied, the root not in registers): read-modify-write backup of the
+        // path (distinct nodes): one lane per path node, the node ids prefetched; a node's depth fixes its
+        // lane, so the slots' updates of a shared ancestor are one lane's program order
+        for (int k = lane; k < plen; k += P) {
+          const size_t idx = nb + (k < P ? s_pnode[grp][j][k] : v.pnode[(size_t)ps * G::MAXD + k]);
+          nd_n<P>(v, idx) += 1;
+          nd_w<P>(v, idx) += val;
+          nd_vl<P>(v, idx) -= 1;
+        }
+        if (lane == 0) {
+          nd_vm<P>(v, bb + blk) = vmnew;
+          nd_c<P>(v, nb + leaf) = blk;
+          nd_n<P>(v, nb + leaf) += 1;
+          nd_w<P>(v, nb + leaf) += val;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      } else {
+        // with sims in this launch: the root and its children from the registers (TreeRoot), deeper path
+        // nodes and the leaf from their block copies when copied (write-through), else read-modify-write in
+        // global memory after a fence if an uncopied store is outstanding (BlockCache)
+        if (lane == 0) nd_vm<P>(v, bb + blk) = vmnew;
+        if (bc.insert_new(blk, lane, pnew, vmnew) == kUncached) bc.dirty = true;
+        const int a1 = plen > 1 ? s_pnode[grp][j][1] - R.cb * P : 0;  // path node 1: root child a1
+        const int r1n = __shfl(R.cn, gbase + a1, 64), r1vl = __shfl(R.cvl, gbase + a1, 64);
+        const double r1w = __shfl(R.cw, gbase + a1, 64);
+        bc.fence_if_dirty();
+        int unc = 0;
+        for (int k = lane; k < plen; k += P) {
+          const int nk = k < P ? s_pnode[grp][j][k] : v.pnode[(size_t)ps * G::MAXD + k];
+          const size_t idx = nb + nk;
+          if (k == 0) {  // the root
+            nd_n<P>(v, idx) = R.n + 1;
+            nd_w<P>(v, idx) = R.w + val;
+            nd_vl<P>(v, idx) = R.vl - 1;
+          } else if (k == 1) {  // root child a1
+            nd_n<P>(v, idx) = r1n + 1;
+            nd_w<P>(v, idx) = r1w + val;
+            nd_vl<P>(v, idx) = r1vl - 1;
+          } else {
+            const int ck = bc.find(nk / P);
+            if (ck >= 0) {
+              int32_t &n = bc.template at<int32_t>(ck, NodeRec<P>::N, nk % P);
+              double &w = bc.template at<double>(ck, NodeRec<P>::W, nk % P);
+              int32_t &vl = bc.template at<int32_t>(ck, NodeRec<P>::VL, nk % P);
+              const int32_t n1 = n + 1, vl1 = vl - 1;
+              const double w1 = w + val;
+              n = n1;
+              w = w1;
+              vl = vl1;
+              nd_n<P>(v, idx) = n1;
+              nd_w<P>(v, idx) = w1;
+              nd_vl<P>(v, idx) = vl1;
+            } else {
+              nd_n<P>(v, idx) += 1;
+              nd_w<P>(v, idx) += val;
+              nd_vl<P>(v, idx) -= 1;
+              unc = 1;
+            }
+          }
+        }
+        // the leaf: a root child (plen 1, registers: lane la), or a deeper node
+        const int la = leaf - R.cb * P;
+        if (plen == 1) {
+          if (lane == la) {
+            nd_c<P>(v, nb + leaf) = blk;
+            nd_n<P>(v, nb + leaf) = R.cn + 1;
+            nd_w<P>(v, nb + leaf) = R.cw + val;
+          }
+        } else {
+          const int cl = bc.find(leaf / P);  // group-uniform
+          if (lane == 0) {
+            if (cl >= 0) {
+              bc.template at<int32_t>(cl, NodeRec<P>::C, leaf % P) = blk;
+              int32_t &n = bc.template at<int32_t>(cl, NodeRec<P>::N, leaf % P);
+              double &w = bc.template at<double>(cl, NodeRec<P>::W, leaf % P);
+              const int32_t n1 = n + 1;
+              const double w1 = w + val;
+              n = n1;
+              w = w1;
+              nd_c<P>(v, nb + leaf) = blk;
+              nd_n<P>(v, nb + leaf) = n1;
+              nd_w<P>(v, nb + leaf) = w1;
+            } else {
+              nd_c<P>(v, nb + leaf) = blk;
+              nd_n<P>(v, nb + leaf) += 1;
+              nd_w<P>(v, nb + leaf) += val;
+            }
+          }
+          unc |= cl == kUncached;
+        }
+        if (group_or<P>(unc)) bc.dirty = true;
       }
       if (lane == 0) {
-        nd_vm<P>(v, bb + blk) = legal_mask<G>(Board{lpos, lneg});
-        nd_c<P>(v, nb + leaf) = blk;
-        nd_n<P>(v, nb + leaf) += 1;
-        nd_w<P>(v, nb + leaf) += val;
         v.used[tree] = blk + 1;
         v.need[ps] = 0;
       }
@@ -1454,12 +1788,16 @@ __device__ __forceinline__ void expand_vl_body(View v, const float *probs0, cons
           R.cw += val;
         }
       }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-      if (refill && fill_slot_vl<G>(v, tree, j, limit, started, R, rng, terr, pl, noise, nz, sc) == SIM_ERROR)
+      if (refill && fill_slot_vl<G, S>(v, tree, j, limit, started, R, rng, terr, pl, noise, nz, sc, bc) == SIM_ERROR)
         return;
     }
   }
-  if (lane == 0) sc.flush(v.cnt + (size_t)tree * C_NCNT);
+  if (lane == 0) {
+#ifdef SPMCTS_TREE_PROF
+    sc.prof_flush(8);
+#endif
+    sc.flush(v.cnt + (size_t)tree * C_NCNT);
+  }
   if (refill && lane == 0) {
     v.tstarted[tree] = started;
     if (terr) set_err(v, SPMCTS_ERR_TAPE);
@@ -2232,7 +2570,7 @@ int spmcts_arena_create(const spmcts_config *cfg, int device, spmcts_arena **out
     return rc;
   }
 #ifndef SPMCTS_AB
-  for (const char *n : {"SPMCTS_TREE_BLOCK", "SPMCTS_EXPAND_CO"})
+  for (const char *n : {"SPMCTS_TREE_BLOCK", "SPMCTS_EXPAND_CO", "SPMCTS_TREE_COPIES"})
     if (getenv(n)) {
       delete h;
       return fail(SPMCTS_ERR_AB_SWITCH, std::string(n) + " is a switch of the A/B library (make ab: libspmcts_ab.so)");
@@ -2362,6 +2700,26 @@ static int launch_rows(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_de
   return 0;
 }
 
+#ifdef SPMCTS_AB
+// SPMCTS_TREE_COPIES=1 (A/B library): the threaded tree kernels with 16 LDS block copies per tree
+static bool tree_copies() {
+  static const bool v = getenv("SPMCTS_TREE_COPIES") && strcmp(getenv("SPMCTS_TREE_COPIES"), "1") == 0;
+  return v;
+}
+#endif
+
+#ifdef SPMCTS_TREE_PROF
+// the per-phase cycle sums of the tree kernels since the last reset (g_tprof), into out[16]
+extern "C" int spmcts_ab_tree_prof(unsigned long long *out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tprof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+  if (reset) {
+    static const unsigned long long zero[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_tprof), zero, sizeof(zero)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
+
 int spmcts_select_tree(spmcts_arena *h, spmcts_stream stream) {
   if (!h) return fail(-1, "null arena");
   hipStream_t s = (hipStream_t)stream;
@@ -2373,6 +2731,8 @@ int spmcts_select_tree(spmcts_arena *h, spmcts_stream stream) {
 #ifdef SPMCTS_AB
       if (tb > 64)
         DISPATCH(h, hipLaunchKernelGGL((k_select_vl<GG, 512>), dim3(nblk(n, tpb)), dim3(tb), 0, s, h->v, n));
+      else if (tree_copies())
+        DISPATCH(h, hipLaunchKernelGGL((k_select_vl<GG, 64, 16>), dim3(nblk(n, tpb)), dim3(tb), 0, s, h->v, n));
       else
 #endif
         DISPATCH(h, hipLaunchKernelGGL(k_select_vl<GG>, dim3(nblk(n, tpb)), dim3(tb), 0, s, h->v, n));
@@ -2415,6 +2775,9 @@ int spmcts_expand2(spmcts_arena *h, const float *probs0_dev, const float *values
                                      h->v, probs0_dev, values0_dev, probs1_dev, values1_dev));
     else if (tb > 64)
       DISPATCH(h, hipLaunchKernelGGL((k_expand_vl<GG, 512>), dim3(nblk(h->v.T, tpb)), dim3(tb), 0, (hipStream_t)stream,
+                                     h->v, probs0_dev, values0_dev, probs1_dev, values1_dev));
+    else if (tree_copies())
+      DISPATCH(h, hipLaunchKernelGGL((k_expand_vl<GG, 64, 16>), dim3(nblk(h->v.T, tpb)), dim3(tb), 0, (hipStream_t)stream,
                                      h->v, probs0_dev, values0_dev, probs1_dev, values1_dev));
     else
 #endif

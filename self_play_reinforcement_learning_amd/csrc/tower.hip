@@ -1632,7 +1632,8 @@ static int ab_switch_guard() {
 #else
   static const int rc = [] {
     for (const char *n : {"SPMCTS_TOWER_CG", "SPMCTS_TOWER_RING", "SPMCTS_TOWER_C256", "SPMCTS_WIDE_TAILS", "SPMCTS_HEADS",
-                          "SPMCTS_HEADS_C256", "SPMCTS_TREE_BLOCK", "SPMCTS_EXPAND_CO", "SPMCTS_TOWER_M16"})
+                          "SPMCTS_HEADS_C256", "SPMCTS_TREE_BLOCK", "SPMCTS_EXPAND_CO", "SPMCTS_TOWER_M16",
+                          "SPMCTS_TREE_COPIES"})
       if (getenv(n)) return SPMCTS_ERR_AB_SWITCH;
     return 0;
   }();
