@@ -97,7 +97,8 @@ __device__ __forceinline__ void conv_tap(const char *src, const Nbr<K> &nb, f32x
 #pragma unroll
   for (int k = 0; k < KK32; ++k) {
     const int s = TAP * KK32 + k;
-    if (k + 1 < KK32) {
+    if (K::ABL & 8) {  // timing ablation (A/B library only, wrong results): no LDS operand reads
+    } else if (k + 1 < KK32) {
 #pragma unroll
       for (int t = 0; t < K::NT; ++t)
         if ((LV >> t) & 1u) {
@@ -119,7 +120,8 @@ __device__ __forceinline__ void conv_tap(const char *src, const Nbr<K> &nb, f32x
 #pragma unroll
     for (int mm = 0; mm < NM; ++mm) acur[mm] = a[slot][mm];
     const int sn = s + DEPTH;
-    if (sn < STEPS) {
+    if (K::ABL & 16) {  // timing ablation (A/B library only, wrong results): no weight loads in the k-loop
+    } else if (sn < STEPS) {
 #pragma unroll
       for (int mm = 0; mm < NM; ++mm) a[slot][mm] = wb.load(wl_off + mm * MSTRIDE + (uint32_t)sn * 1024u);
     } else if (kRingAlways || sn - STEPS < wn_steps) {
