@@ -1,3 +1,4 @@
+# (A/B code 1612 and the per-pair B pipeline were removed after this measurement: profiles/r05/m16_ablation/)
 # Round 5: the C = 128 trunk on 12-board one-buffer 16x16x32 tiles (tower_wide16.h, A/B code 1612: each weight
 # fragment for 16 MFMAs) -- bit-equality with the shipped two-buffer trunk (1602 = the product schedule in the
 # A/B library), then trunk-only timing 6,144 boards bf16, alternated.

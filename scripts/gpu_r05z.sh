@@ -1,3 +1,4 @@
+# (A/B code 1612 and the per-pair B pipeline were removed after this measurement: profiles/r05/m16_ablation/)
 # Round 5: wide16 with the B operands pipelined per (k-step, tile) pair (tap_pairs: 0 spills at C = 256, was 9-20):
 # (1) C = 256 outputs bit-equal to the previous product library (2 and 20 blocks, host + device-count paths, bf16
 # and fp16); (2) the C = 128 12-board code 1612 bit-equal to the two-buffer trunk (1602); (3) trunk-only timing:
