@@ -1593,9 +1593,10 @@ static bool wide_tails3() {  // SPMCTS_WIDE_TAILS=3: C = 256 launches with 3-boa
 }
 // the C = 256 Connect4 trunk on the 16x16x32 one-buffer tiles (tower_wide16.h, its M16 weight layout) unless
 // SPMCTS_TOWER_C256 (=32: round 4's 32x32x16 one-buffer tiles; =3: the 3-board tiles), SPMCTS_WIDE_TAILS or a
-// SPMCTS_TOWER_CG probe code (all on the 32x32x16 layout) selects another set
-static bool c256_m16() {
-  static const bool v = !getenv("SPMCTS_TOWER_C256") && !getenv("SPMCTS_WIDE_TAILS") && !getenv("SPMCTS_TOWER_CG");
+// SPMCTS_TOWER_CG probe code other than 25xx (all on the 32x32x16 layout) selects another set
+static bool c256_m16() {  // (SPMCTS_TOWER_CG codes 25xx are variants of the 16x16x32 C = 256 trunk)
+  static const bool cg25 = getenv("SPMCTS_TOWER_CG") && atoi(getenv("SPMCTS_TOWER_CG")) / 100 == 25;
+  static const bool v = !getenv("SPMCTS_TOWER_C256") && !getenv("SPMCTS_WIDE_TAILS") && (!getenv("SPMCTS_TOWER_CG") || cg25);
   return v;
 }
 static bool heads_co256() {  // SPMCTS_HEADS_C256=lds: the LDS-staged C = 256 linear heads
@@ -1812,6 +1813,14 @@ static int forward_ab(int32_t width, int32_t height, int32_t channels, int32_t n
   if (width == 7 && height == 6 && channels == 256 && cg == 2300)
     return launch_split<Cfg<256, 256, 7, 6, 4, 4, 0, 2, 1, true, true, __bf16, true>, Cfg<256, 128, 7, 6, 4>,
                         Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+  // the 16x16x32 one-buffer C = 256 trunk (tower_wide16.h, the product's) and two variants: a 4-deep weight ring
+  // (2564), the compiler's own k-loop schedule (2556)
+  if (width == 7 && height == 6 && channels == 256 && cg == 2560)
+    return launch<Cfg<256, 256, 7, 6, 4, 4, 0, 2, 1, true, true, __bf16, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+  if (width == 7 && height == 6 && channels == 256 && cg == 2564)
+    return launch<Cfg<256, 256, 7, 6, 4, 4, 0, 4, 1, true, true, __bf16, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+  if (width == 7 && height == 6 && channels == 256 && cg == 2556)
+    return launch<Cfg<256, 256, 7, 6, 4, 4, 256, 2, 1, true, true, __bf16, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
   if (width == 7 && height == 6 && channels == 256 && cg == 254)  // the one-buffer trunk with a 4-deep weight ring
     return launch_split<Cfg<256, 256, 7, 6, 4, 4, 0, 4, 1, true, true, __bf16, true>, Cfg<256, 128, 7, 6, 4>,
                         Cfg<256, 128, 7, 6, 4>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
