@@ -166,7 +166,7 @@ def lib():
                 # a build from before this entry point existed (SPMCTS_LIB pointing at an earlier library for a
                 # same-box A/B): only the entry points it has are bound; the product library exports every
                 # symbol the header declares (tests/test_native_lib.py)
-                if LIB_PATH == _DEFAULT_LIB:
+                if os.path.realpath(LIB_PATH) == os.path.realpath(_DEFAULT_LIB):
                     raise
                 continue
             f.argtypes = args

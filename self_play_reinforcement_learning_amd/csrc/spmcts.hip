@@ -1020,8 +1020,9 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
       if (ncs >= 0) bc.template at<int32_t>(ncs, NodeRec<P>::VL, node % P) = node_vl;
     }
     // the global store of the path's virtual loss waits for the sim's end (one store per path node, all
-    // at once): gfx950's vmcnt counts stores too, so a store here would hold up the next level's loads
-    if (ncs == kUncached) bc.dirty = true;
+    // at once): gfx950's vmcnt counts stores too, so a store here would hold up the next level's loads.
+    // `dirty` is set where those stores are issued (leak, pending, terminal below), not here: nothing of
+    // this sim is in flight yet, so the levels of one sim read without a fence.
     if (depth == 1 && lane == a0) R.cvl = node_vl;  // the root child's vl, in registers too
     if (cb < 0) {
       if (lane == 0) set_err(v, SPMCTS_ERR_STATE);
@@ -1089,7 +1090,12 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
       score = (player > 0 ? q : -q) + u;
     }
     if (!group_or<P>(valid ? 1 : 0)) {  // mcts.py:349-354: return, virtual loss left in place
-      for (int k = lane; k <= depth; k += P) nd_vl<P>(v, nb + pl.node[k]) = pl.vl[k];
+      int unc = 0;
+      for (int k = lane; k <= depth; k += P) {
+        nd_vl<P>(v, nb + pl.node[k]) = pl.vl[k];
+        unc |= pl.cs[k] == kUncached;
+      }
+      if (group_or<P>(unc)) bc.dirty = true;
       sc.leak += 1;
       return SIM_LEAK;
     }
@@ -1156,11 +1162,14 @@ __device__ int sim_vl(const View &v, int tree, int j, TreeRoot &R, TreeRng &rng,
         sc.term += 1;
       } else {
         const size_t pb = (size_t)ps * G::MAXD;
+        int unc = 0;
         for (int k = lane; k <= depth; k += P) {
           const int nk = pl.node[k];
           v.pnode[pb + k] = nk;
           nd_vl<P>(v, nb + nk) = pl.vl[k];
+          unc |= pl.cs[k] == kUncached;
         }
+        if (group_or<P>(unc)) bc.dirty = true;
       }
       sc.sims += 1;
       sc.depth += depth + 1;
@@ -1261,7 +1270,9 @@ __global__ __launch_bounds__(TB) void k_select_vl(View v, int n_active) {
   const int kt = v.tK[tree];  // this tree's sims in flight (its own thread_count, <= K)
   for (int j = 0; j < kt; ++j) {
     if (v.need[tree * v.K + j]) continue;
-    if (fill_slot_vl<G, S>(v, tree, j, limit, started, R, rng, terr, pl, noise, nz, sc, bc) == SIM_ERROR) return;
+    // SIM_ERROR (a corrupt tree: the sticky SPMCTS_ERR_STATE flag is set) ends the tree's launch; the counters
+    // of the sims completed before it are still flushed below (the failing sim's path vl is not written)
+    if (fill_slot_vl<G, S>(v, tree, j, limit, started, R, rng, terr, pl, noise, nz, sc, bc) == SIM_ERROR) break;
   }
   if (lane == 0) {
 #ifdef SPMCTS_TREE_PROF
@@ -1654,9 +1665,9 @@ __device__ __forceinline__ void expand_vl_body(View v, const float *probs0, cons
       const int mover = __shfl(my_mover, gbase + j, 64);
       const uint64_t lpos = __shfl(my_pos, gbase + j, 64), lneg = __shfl(my_neg, gbase + j, 64);
       const int blk = used;
-      if (blk >= v.cap) {
+      if (blk >= v.cap) {  // sticky SPMCTS_ERR_POOL; the counters of the slots done so far are still flushed
         if (lane == 0) set_err(v, SPMCTS_ERR_POOL);
-        return;
+        break;
       }
       ++used;
       const float pnew = lane < G::A ? s_pr[grp][j][lane] : 0.f;
@@ -1789,7 +1800,7 @@ __device__ __forceinline__ void expand_vl_body(View v, const float *probs0, cons
         }
       }
       if (refill && fill_slot_vl<G, S>(v, tree, j, limit, started, R, rng, terr, pl, noise, nz, sc, bc) == SIM_ERROR)
-        return;
+        break;  // sticky SPMCTS_ERR_STATE; counters flushed below
     }
   }
   if (lane == 0) {

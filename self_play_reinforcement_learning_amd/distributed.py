@@ -288,6 +288,16 @@ def check_devices(n):
     return have
 
 
+def assert_gpu_untouched(what):
+    """The parent of N rank processes must not have initialised HIP: a GPU-initialised process may
+    start children but never exec, and its own device context would sit on GPU 0 beside rank 0's for the
+    whole job.  Raises RuntimeError if it has (torch.cuda.is_initialized(): device counting does not
+    initialise, any allocation or kernel does)."""
+    if torch.cuda.is_initialized():
+        raise RuntimeError(f"{what}: this process has already initialised the GPU; start the rank processes "
+                           f"before any GPU call (bench.py --gpus N and SelfPlayScheduler(gpus=N) do)")
+
+
 def launch_script(argv, n, poll=0.2):
     """Run `python argv` as n ranks of a single-node job (bench.py --gpus N without torchrun): each
     child gets RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* as torchrun would set them.  Must be called
@@ -296,6 +306,7 @@ def launch_script(argv, n, poll=0.2):
     import subprocess
     import sys
 
+    assert_gpu_untouched("launch_script")
     port = free_port()
     procs = [subprocess.Popen([sys.executable] + list(argv), env=rank_env(r, n, port)) for r in range(n)]
     rc = 0
@@ -333,6 +344,7 @@ def spawn_ranks(fn, n, *args, timeout=None, **kwargs):
     import multiprocessing as mp
     from multiprocessing.connection import wait
 
+    assert_gpu_untouched("spawn_ranks")
     ctx = mp.get_context("spawn")
     port = free_port()
     procs = [ctx.Process(target=_spawned_rank, args=(r, n, port, fn, args, kwargs)) for r in range(n)]

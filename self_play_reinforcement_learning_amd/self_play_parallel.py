@@ -227,6 +227,9 @@ class SelfPlayScheduler:
         (updateworker.py:76-78); here that is a warning and the ring stays empty."""
         from glob import glob
 
+        if not self.save_dir:
+            logging.warning("resume_memory: no save_dir; starting from an empty replay")
+            return None
         runs = sorted(d for d in glob(os.path.join(self.save_dir, "*")) if os.path.isdir(d)
                       and (not prev_run or os.path.basename(d) != self.start_time) and os.listdir(d))
         saves = sorted(glob(os.path.join(runs[-1], "memory*"))) if runs else []
@@ -247,6 +250,8 @@ class SelfPlayScheduler:
     def _load_latest(self, prev_run=False):
         from glob import glob
 
+        if not self.save_dir:
+            return None
         runs = sorted(d for d in glob(os.path.join(self.save_dir, "*")) if os.path.isdir(d)
                       and (not prev_run or os.path.basename(d) != self.start_time) and os.listdir(d))
         if not runs:

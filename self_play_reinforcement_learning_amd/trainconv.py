@@ -111,16 +111,25 @@ def _forward(conv, x):
     return Conv3x3.apply(x, conv.weight, conv.bias)
 
 
+# Channel counts the trainer routes by default: the ones whose graphed step was timed against MIOpen
+# (ResNet-128: 3.26 vs ~5 ms, profiles/r04/trainer/).  The kernels also take C = 256 (checked for
+# correctness in tests/test_gpu_trainconv.py), but there k_conv3x3 holds its whole A operand in registers
+# (9 x 8 f16x8 = 288 VGPRs) and spills, and no step A/B exists: channels=(128, 256) opts in.
+MEASURED_CHANNELS = (128,)
+
+
 @contextlib.contextmanager
-def hip_block_convs(network, enabled=True):
+def hip_block_convs(network, enabled=True, channels=MEASURED_CHANNELS):
     """Within the block, the residual blocks' 3x3 convolutions of `network` (a ResidualTower on a CUDA
     device, run under fp16 autocast) go through Conv3x3.  Yields whether they do (False: unsupported
-    shape, another module type, or not enabled -- the module's own convolutions run)."""
+    shape or padding mode, a channel count outside `channels`, another module type, or not enabled --
+    the module's own convolutions run)."""
     blocks = getattr(network, "residual_blocks", None)
     convs = [] if blocks is None else [c for blk in blocks for c in (blk.conv1, blk.conv2)]
     ok = (enabled and convs and all(
         isinstance(c, torch.nn.Conv2d) and c.kernel_size == (3, 3) and c.stride == (1, 1) and c.padding == (1, 1)
-        and c.groups == 1 and c.dilation == (1, 1) and c.weight.is_cuda for c in convs)
+        and c.padding_mode == "zeros" and c.groups == 1 and c.dilation == (1, 1) and c.weight.is_cuda
+        and c.in_channels in channels and c.out_channels in channels for c in convs)
         and all(supported(network.width, network.height, c.in_channels, c.out_channels) for c in convs))
     if not ok:
         yield False

@@ -39,6 +39,12 @@ threads can expand the same leaf and the second replaces the first one's childre
 one game thread this is rare; with 8 game threads contending for the GIL it is frequent,
 and it measurably flattens the root visit distribution.
 
+Round 6: resnet_eval is the arena's search (BASELINE config 5): the same threaded pipeline with
+`MCTreeSearch.evaluate(True)` on both the tree and its _play — root noise still on (mcts.py:323-327), the
+move drawn from n^20 (temp/20, mcts.py:273-276; selfplayworker.py:71-81 sets evaluate on both arena
+policies).  Each sample also records the root visit counts.  Made in parts by tests/golden/run_g6_eval.sh
+and merged with `merge resnet_eval <parts...>`.
+
 Only inputs and the outputs the reference produced are written (no reference source).
 
 Round 3: resnet_single holds 1,000 searches per position (was 160), made with one process per
@@ -110,16 +116,19 @@ def _resnet():
     return net, {k: float(v.double().sum()) for k, v in sd.items()}
 
 
-def _search_once(MCTreeSearch, Connect4Env, network, opening, thread_count):
+def _search_once(MCTreeSearch, Connect4Env, network, opening, thread_count, evaluate=False):
     tree = MCTreeSearch(network=network, env=Connect4Env, iterations=SIMS, thread_count=thread_count)
     for a in opening:
         tree.play_action(a, None)
     tree.train(False)
-    tree.evaluate(False)
+    tree.evaluate(evaluate)
     action = tree()
     mv = tree.temp_memory[-1]
-    return dict(tree_probs=mv.tree_probs.numpy().astype(float).tolist(), action=int(action), q=float(mv.q),
-                root_n=int(tree.root_node.n))
+    out = dict(tree_probs=mv.tree_probs.numpy().astype(float).tolist(), action=int(action), q=float(mv.q),
+               root_n=int(tree.root_node.n))
+    if evaluate:  # tree_probs are n^20 there (mcts.py:273-276): keep the visit counts as well
+        out["visits"] = [int(c.n) for c in tree.root_node.children]
+    return out
 
 
 class _ReexpansionCounter:
@@ -149,7 +158,7 @@ class _ReexpansionCounter:
         return dict(expansions=self.calls, re_expansions=self.re)
 
 
-def run_threaded(net_module, samples, label, game_threads, positions=POSITIONS):
+def run_threaded(net_module, samples, label, game_threads, positions=POSITIONS, evaluate=False):
     """The reference's serving structure: InferenceWorker process + proxy + game threads."""
     from games.algos.inference_proxy import InferenceProxy
     from games.algos.inference_worker import InferenceWorker
@@ -171,7 +180,7 @@ def run_threaded(net_module, samples, label, game_threads, positions=POSITIONS):
             res = []
 
             def job(_):
-                r = _search_once(MCTreeSearch, Connect4Env, proxy, opening, THREADS)
+                r = _search_once(MCTreeSearch, Connect4Env, proxy, opening, THREADS, evaluate)
                 with lock:
                     res.append(r)
                     if len(res) % 20 == 0:
@@ -228,9 +237,9 @@ def _rounded(data):
 def run_part(name, samples, pi, out):
     """One position of a resnet set in its own process (several run side by side on the host's cores;
     `merge` joins the parts): `resnet_single <samples> <position> <out.json>`."""
-    gt = {"resnet_single": 1, "resnet_serving": GAME_THREADS}[name]
+    gt = {"resnet_single": 1, "resnet_serving": GAME_THREADS, "resnet_eval": 1}[name]
     net, sums = _resnet()
-    pos = run_threaded(net, samples, f"{name}[{pi}]", gt, positions=[POSITIONS[pi]])
+    pos = run_threaded(net, samples, f"{name}[{pi}]", gt, positions=[POSITIONS[pi]], evaluate=name == "resnet_eval")
     json.dump(dict(threads_per_worker=gt, net_checksums=sums, pi=pi, position=pos[0]), open(out, "w"))
 
 
@@ -255,8 +264,13 @@ def merge(name, parts, append=False):
         cur["samples"] = cur["samples"] + pos["samples"]
         cur["expansions"] += pos["expansions"]
         cur["re_expansions"] += pos["re_expansions"]
-    assert sorted(by_pi) == list(range(len(by_pi))), sorted(by_pi)
+    if name == "resnet_eval":  # a subset of the positions: each entry keeps its POSITIONS index
+        for pi, cur in by_pi.items():
+            cur["pi"] = pi
+    else:
+        assert sorted(by_pi) == list(range(len(by_pi))), sorted(by_pi)
     data[name] = dict(sims=SIMS, thread_count=THREADS, game="connect4", threads_per_worker=ps[0]["threads_per_worker"],
+                      evaluate=name == "resnet_eval",
                       net="ResidualTower(7,6,7,num_blocks=20,filter_factor=32) seed 0",
                       net_checksums=ps[0]["net_checksums"], positions=[by_pi[i] for i in sorted(by_pi)])
     json.dump(_rounded(data), open(OUT, "w"), separators=(",", ":"))

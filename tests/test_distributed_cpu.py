@@ -1,4 +1,4 @@
-"""CPU: the multi-GPU exchange steps with torch.distributed gloo, world sizes 2 and 4: the
+"""CPU: the multi-GPU exchange steps with torch.distributed gloo, world sizes 2, 4 and 8: the
 episode-batch MoveExchange (Move rows staged per rank, one header all_gather + one gather to rank 0
 per round, statistics summed in the same round), the engines' play_games loops that end on it,
 the primitives (stats all_reduce, max, one-buffer weight broadcast), and the self-launch helpers that
@@ -132,7 +132,7 @@ def _loop_worker(rank, world, port, q):
     torch.distributed.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_play_games_keeps_ranks_in_step_gloo(world):
     """Ranks that finish their share early keep stepping idle plies until an exchange round finds
     every rank done (so the rounds always match, no deadlock); every finished game's records reach
@@ -339,7 +339,7 @@ def test_pack_unpack_roundtrip():
         assert torch.equal(back[k].reshape(m[k].shape), m[k]), k
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_exchange_primitives_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -537,7 +537,7 @@ def _exchange_worker(rank, world, port, q):
     torch.distributed.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [1, 2, 4])
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
 def test_move_exchange_rounds_gloo(world):
     """Rounds every 3 plies (+ one forced): None between rounds; at a round every rank sees the
     same (all-done, summed stats); rank 0 receives exactly the rows staged since the previous round,
@@ -609,3 +609,17 @@ def test_scheduler_rank_count_and_spawn_kwargs(tmp_path, monkeypatch):
     assert kw["network"] is not net and torch.equal(kw["network"].conv1.weight, net.conv1.weight)
     assert kw["evaluation_policy_container"].policy_kwargs["iterations"] == 10
     assert isinstance(kw["evaluation_policy_container"].policy_kwargs["network"], ResidualTower)
+
+
+def test_launchers_refuse_a_gpu_initialised_parent(monkeypatch):
+    """launch_script / spawn_ranks start the rank processes only from a parent that has not initialised HIP
+    (bench.py --gpus N, SelfPlayScheduler(gpus=N)); with torch.cuda.is_initialized() True they raise before
+    starting anything."""
+    monkeypatch.setattr(torch.cuda, "is_initialized", lambda: True)
+    with pytest.raises(RuntimeError, match="initialised the GPU"):
+        D.launch_script(["-c", "raise SystemExit(3)"], 2)
+    with pytest.raises(RuntimeError, match="initialised the GPU"):
+        D.spawn_ranks(print, 2)
+    monkeypatch.undo()
+    assert not torch.cuda.is_initialized()
+    assert D.launch_script(["-c", "raise SystemExit(0)"], 2) == 0

@@ -79,6 +79,16 @@ def test_hip_block_convs_patch_is_scoped():
     small = ResidualTower(7, 6, 7, num_blocks=1, filter_factor=16).cuda()
     with hip_block_convs(small) as on:
         assert not on
+    # C = 256 runs only when asked for (no step A/B against MIOpen at that width, trainconv.MEASURED_CHANNELS)
+    wide = ResidualTower(7, 6, 7, num_blocks=1, filter_factor=64).cuda()
+    with hip_block_convs(wide) as on:
+        assert not on
+    with hip_block_convs(wide, channels=(128, 256)) as on:
+        assert on
+    # the kernels zero-pad: a conv with another padding mode keeps its own forward
+    net.residual_blocks[1].conv2.padding_mode = "reflect"
+    with hip_block_convs(net) as on:
+        assert not on and "forward" not in vars(net.residual_blocks[0].conv1)
 
 
 def test_trainer_hip_convs_match_miopen_step():

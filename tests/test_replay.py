@@ -178,3 +178,20 @@ def test_scheduler_resume_memory(tmp_path):
     assert b.trainer.memory_size == 5000
     # training starts at once from the resumed ring (min_memory met)
     assert b.trainer.step() is not None
+
+
+def test_scheduler_resume_memory_without_save_dir():
+    """resume_memory / resume_model with save_dir=None: a warning and an empty ring (as with no snapshot),
+    not a TypeError from the glob."""
+    from self_play_reinforcement_learning_amd.envs import Connect4Env
+    from self_play_reinforcement_learning_amd.mcts import MCTreeSearch
+    from self_play_reinforcement_learning_amd.modules import ResidualTower
+    from self_play_reinforcement_learning_amd.base_model import ModelContainer
+    from self_play_reinforcement_learning_amd.self_play_parallel import SelfPlayScheduler
+
+    net = ResidualTower(7, 6, 7, num_blocks=1, filter_factor=2)
+    c = ModelContainer(MCTreeSearch, policy_kwargs=dict(env=Connect4Env, iterations=10, memory_size=500,
+                                                        min_memory=10))
+    s = SelfPlayScheduler(c, Connect4Env, network=net, save_dir=None, device="cpu", evaluation_games=0)
+    s.setup_update_worker(resume_memory=True, resume_model=True)
+    assert len(s.trainer.memory) == 0
