@@ -43,11 +43,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 TRAFFIC_FILE = os.path.join(HERE, "profiles", "r01_bench_prof", "k_tower_traffic.json")  # --search-threads 1
-TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r05_bench_prof", "k_tower_traffic.json")  # 4 (default)
+TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r06_bench_prof", "k_tower_traffic.json")  # 4 (default)
 TREE_TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r05_tree_pmc", "tree_traffic.json")
-# in-bench clock and MFMA-busy share of the timed k_tower_dyn dispatches (one PMC pass per trunk dtype,
-# scripts/gpu_prof_r04.sh -> scripts/tower_util.py): the roofline's frac = busy x clock / 2.4 GHz / 0.833
-CLOCK_FILES = {d: os.path.join(HERE, "profiles", "r05_bench_prof", f"tower_util_bench_{d}.json") for d in ("fp16", "bf16")}
+# in-bench MFMA-busy share (and profiled clock) of the timed k_tower_dyn dispatches (one PMC pass per trunk dtype,
+# scripts/gpu_r06a.sh -> scripts/tower_util.py): the roofline's frac ~ busy x clock / 2.4 GHz / 0.833
+CLOCK_FILES = {"fp16": os.path.join(HERE, "profiles", "r06_bench_prof", "tower_util_bench_fp16.json"),
+               "bf16": os.path.join(HERE, "profiles", "r05_bench_prof", "tower_util_bench_bf16.json")}
 
 # MI355X reference figures (/opt/skills/guides/MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
@@ -62,6 +63,82 @@ def resnet_flops_per_leaf(W, H, A, filter_factor, num_blocks):
     f += 2 * (2 * C * ff * cells)  # two 1x1 head convs
     f += 2 * ff * cells * A + 2 * ff * cells * 8 * ff + 2 * 8 * ff
     return f
+
+
+def executed_trunk_flops_per_leaf(W, H, filter_factor, num_blocks):
+    """MFMA FLOPs the fused trunk ISSUES per board (C4 edge-tile layout, csrc/tower_edge.h): every conv3x3
+    of the residual blocks skips the 12 of 72 (cell tile, tap) pairs whose taps read zero padding only
+    (5/6 of the dense MFMAs run); the stem (3 input planes, all 9 taps) and the 1x1 head convs run dense.
+    (A batch's one partly empty tail tile issues MFMAs for its empty board slots too; they are not counted.)"""
+    C, ff, cells = 4 * filter_factor, filter_factor, W * H
+    return 2 * 9 * 3 * C * cells + 2 * num_blocks * (2 * 9 * C * C * cells) * 5 / 6 + 2 * (2 * C * ff * cells)
+
+
+class GfxClock:
+    """The GPU's graphics clock over the timed region, measured in THIS run: a background thread reads
+    amdsmi's gpu_metrics (current_gfxclks of the XCDs, MHz) every `period` seconds between start() and
+    stop() and reports their mean.  The timed region is >= 95 % trunk dispatches, so the mean is the clock
+    the trunk ran at; the roofline's frac_at_clock = achieved / (peak x clock / 2.4 GHz)."""
+
+    def __init__(self, device, period=0.01):
+        import threading
+
+        self.samples, self.err, self.period = [], None, period
+        self._stop = threading.Event()
+        self._thread = None
+        try:
+            import amdsmi
+            import torch
+
+            amdsmi.amdsmi_init()
+            self._smi = amdsmi
+            pr = torch.cuda.get_device_properties(device)
+            bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+            self.bdf = bdf
+            self._h = amdsmi.amdsmi_get_processor_handle_from_bdf(bdf)
+            self._read()  # fail here, not in the thread
+        except Exception as e:  # report the reason in the line; the bench still runs
+            self.err = f"{type(e).__name__}: {e}"
+
+    def _read(self):
+        m = self._smi.amdsmi_get_gpu_metrics_info(self._h)
+        clks = m.get("current_gfxclks")
+        vals = [c for c in (clks if isinstance(clks, (list, tuple)) else []) if isinstance(c, (int, float)) and 0 < c < 65535]
+        if not vals and isinstance(m.get("current_gfxclk"), (int, float)):
+            vals = [m["current_gfxclk"]]
+        act = m.get("gfx_activity")
+        return (sum(vals) / len(vals) if vals else None), (act if isinstance(act, (int, float)) and act <= 100 else None)
+
+    def _run(self):
+        while not self._stop.is_set():
+            try:
+                self.samples.append(self._read())
+            except Exception as e:
+                self.err = f"{type(e).__name__}: {e}"
+                return
+            self._stop.wait(self.period)
+
+    def start(self):
+        import threading
+
+        if self.err is None:
+            self._thread = threading.Thread(target=self._run, daemon=True)
+            self._thread.start()
+
+    def stop(self):
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join()
+
+    def report(self):
+        clk = [c for c, _ in self.samples if c is not None]
+        act = [a for _, a in self.samples if a is not None]
+        if not clk:
+            return {"clock_ghz": None, "error": self.err or "no gfx clock samples"}
+        return {"clock_ghz": sum(clk) / len(clk) / 1e3, "clock_ghz_min": min(clk) / 1e3, "clock_ghz_max": max(clk) / 1e3,
+                "samples": len(clk), "gfx_activity_pct": sum(act) / len(act) if act else None,
+                "source": f"amdsmi gpu_metrics current_gfxclks (mean over the XCDs), every {self.period * 1e3:.0f} ms "
+                          f"over this run's timed region, device {self.bdf}"}
 
 
 def head_linear_flops(W, H, A, filter_factor):
@@ -242,11 +319,16 @@ def main():
     ap.add_argument("--stagger", action="store_true",
                     help="lane i runs i * S / lanes simulation steps behind lane 0 (engine.LanedEngine stagger) "
                          "instead of the lanes in lock step")
+    ap.add_argument("--no-cross-dedup", action="store_true",
+                    help="lanes > 1: per-lane leaf dedup only (default: a lane-1 leaf whose input lane 0 evaluates in "
+                         "the same simulation step takes lane 0's row, engine.LanedEngine cross_dedup)")
     ap.add_argument("--no-pack", action="store_true",
                     help="lanes > 1: keep round-aligned tower tiles (no SPMCTS_TOWER_PACK)")
     ap.add_argument("--twin-no-dedup", type=int, default=5, metavar="PLIES",
                     help="after the timed region, turn leaf dedup off and time PLIES more plies of the same games "
                          "(every leaf its own row, as the reference): reported as no_dedup_twin")
+    ap.add_argument("--no-clock", action="store_true",
+                    help="do not sample the gfx clock (amdsmi) during the timed region")
     ap.add_argument("--progress", action="store_true",
                     help="one stderr line per untimed ply (long warm-ups, e.g. config 3 in steady state)")
     ap.add_argument("--dtype", choices=["bf16", "fp16"], default="fp16",
@@ -310,7 +392,7 @@ def main():
               blocks_per_tree=args.blocks_per_tree, leaf_dedup=False if args.no_leaf_dedup else None)
     if args.lanes > 1:
         eng = LanedEngine("connect4", net, n_games=args.games, lanes=args.lanes, pack=not args.no_pack,
-                          stagger=args.stagger, **kw)
+                          stagger=args.stagger, cross_dedup=False if args.no_cross_dedup else None, **kw)
     else:
         eng = SelfPlayEngine("connect4", net, n_games=args.games, **kw)
     gathered = []
@@ -338,10 +420,13 @@ def main():
     c0 = eng.counters()
     eng.enable_timers(True)
 
+    gclk = None if args.no_clock else GfxClock(dev)
     D.barrier()
     torch.cuda.synchronize()
     ref = torch.cuda.Event(enable_timing=True)  # time origin of the launch intervals (all lanes' streams)
     ref.record()
+    if gclk is not None:
+        gclk.start()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         one_step()
@@ -350,6 +435,8 @@ def main():
     D.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if gclk is not None:
+        gclk.stop()
     elapsed_max = D.all_reduce_max(elapsed)
 
     c1 = eng.counters()
@@ -422,20 +509,26 @@ def main():
         traffic = tj.get("bytes_per_dispatch", tj["bytes_per_launch"]) * max(1, args.lanes)
         traffic_src = os.path.relpath(tfile, HERE)
 
-    # the committed in-bench PMC pass of this trunk dtype (bench.py cannot run the profiler itself)
-    clock = None
+    # the clock of THIS run's timed region (amdsmi, GfxClock): the peak at that clock and the frac against it
+    clock = gclk.report() if gclk is not None else None
+    if clock is not None and clock.get("clock_ghz"):
+        ghz = clock["clock_ghz"]
+        clock.update(peak_at_clock=BF16_DENSE_PEAK_TFLOPS * ghz / 2.4,
+                     frac_at_clock=tw_tflops / (BF16_DENSE_PEAK_TFLOPS * ghz / 2.4),
+                     note="peak scaled linearly from 2.5 PFLOP/s at 2.4 GHz to the clock this run's timed region held")
+    # MFMA busy share of the trunk from the committed in-bench PMC pass (another run of this command: the
+    # profiler cannot run inside bench.py), for the factorisation frac ~ busy x clock/2.4 / executed share
+    mfma_busy_pmc = None
     cfile = CLOCK_FILES.get(args.dtype)
     if cfile and os.path.exists(cfile) and (args.games, args.sims, args.filter_factor, args.blocks) == (4096, 200, 32, 20):
         with open(cfile) as f:
             cj = json.load(f)
-        ghz, busy = cj["clock_ghz_weighted"], cj["mfma_busy_frac_weighted"]
-        clock = {"clock_ghz": ghz, "mfma_busy_frac": busy, "dispatches": cj.get("dispatches"),
-                 "source": os.path.relpath(cfile, HERE),
-                 "peak_at_clock": BF16_DENSE_PEAK_TFLOPS * ghz / 2.4,
-                 "frac_at_clock": tw_tflops / (BF16_DENSE_PEAK_TFLOPS * ghz / 2.4),
-                 "note": "peak scaled to the clock the chip held under this kernel (GRBM_GUI_ACTIVE / 8 / duration, "
-                         "profiled run of this command); frac ~ busy x clock/2.4 / 0.833 (edge tiles skip 16.7 % of "
-                         "the dense MFMAs)"}
+        mfma_busy_pmc = {"mfma_busy_frac": cj["mfma_busy_frac_weighted"], "clock_ghz": cj["clock_ghz_weighted"],
+                         "dispatches": cj.get("dispatches"), "source": os.path.relpath(cfile, HERE),
+                         "note": "a profiled run of this command (rocprofv3 PMC: SQ_VALU_MFMA_BUSY_CYCLES, "
+                                 "GRBM_GUI_ACTIVE), not this run"}
+    ex_fpl = executed_trunk_flops_per_leaf(7, 6, args.filter_factor, args.blocks)
+    ex_tflops = tw_tflops * ex_fpl / trunk_fpl
 
     out = {
         "metric": f"self-play positions/sec (Connect4, {args.sims} sims/move)",
@@ -462,6 +555,7 @@ def main():
             "lanes_staggered": bool(getattr(eng, "stagger", False)) if args.lanes > 1 else False,
             "search_threads": args.search_threads,
             "leaf_dedup": bool(getattr(eng, "leaf_dedup", False)),
+            "cross_lane_dedup": bool(getattr(eng, "cross_dedup", False)),
         },
         "roofline": {
             "kernel": f"tower::k_tower_dyn (fused ResNet-{4 * args.filter_factor}x{args.blocks} trunk, {args.dtype} MFMA)",
@@ -482,7 +576,12 @@ def main():
                            "duration = their union busy time" if lanes > 1 else "one k_tower_dyn dispatch"),
             "avg_dispatch_us": tw_sum_ms / max(1, tw_dispatches) * 1e3,
             "dispatches": tw_dispatches,
+            "executed": {"achieved": ex_tflops, "frac": ex_tflops / BF16_DENSE_PEAK_TFLOPS,
+                         "flops_per_leaf": ex_fpl,
+                         "note": "MFMA FLOPs the trunk issues (the edge tiles skip the 1/6 of the block convs' "
+                                 "dense MFMAs that multiply zero padding only), same launches and time"},
             "clock": clock,
+            "mfma_busy_pmc": mfma_busy_pmc,
         },
         "tree_roofline": {
             "kernel": ("k_select<C4> + k_expand<C4> (PUCT tree walk, backup)" if args.search_threads <= 1 else
@@ -588,7 +687,7 @@ def main():
         kw2 = dict(kw, dtype={"bf16": torch.bfloat16, "fp16": torch.float16}[other])
         if args.lanes > 1:
             eng2 = LanedEngine("connect4", net, n_games=args.games, lanes=args.lanes, pack=not args.no_pack,
-                               stagger=args.stagger, **kw2)
+                               stagger=args.stagger, cross_dedup=False if args.no_cross_dedup else None, **kw2)
         else:
             eng2 = SelfPlayEngine("connect4", net, n_games=args.games, **kw2)
         ex2 = D.MoveExchange(42, 7, sink=lambda g: None, every=args.exchange_every)

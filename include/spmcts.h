@@ -196,6 +196,23 @@ int spmcts_games_set_record(spmcts_arena *h, int32_t record);
  * leaf receives are unchanged.  Off by default; leave it off for evaluators that give rows of
  * different trees different networks (per-row salts).  Leaf counts then count rows, not leaves. */
 int spmcts_set_leaf_dedup(spmcts_arena *h, int32_t on);
+/* Cross-lane leaf dedup (round 6).  Pair `h` (a follower lane) with `leader` (another arena of the same game,
+ * device and search_threads > 1, both single-network; NULL unpairs): in each simulation step
+ * (spmcts_select / spmcts_leaf_rows, with leaf dedup on in both) a follower's pending leaf whose network input
+ * the leader evaluates in the SAME step takes the leader's row instead of one of its own -- the lanes of
+ * engine.LanedEngine run in lock step, and the reference evaluates every leaf (inference_worker.py:89-119),
+ * so with a deterministic, batch-independent evaluator each leaf's outputs are unchanged.  Contract: per step
+ * the leader's rows are built before the follower's (host order), and the follower's expand is
+ * preceded by spmcts_peer_push; the end-of-ply expansions (spmcts_play_action / spmcts_games_end_ply) stay lane-local.
+ * Leaf counts of the follower count its own rows (the leader-served rows follow them). */
+int spmcts_set_leaf_peer(spmcts_arena *h, spmcts_arena *leader);
+/* Before a follower's expand of a simulation step: on leader_stream (after the leader's network outputs of
+ * the step) the leader's rows are copied into the follower's leader-served rows of probs_dev / values_dev
+ * (k_peer_push), and `stream` waits for them (events).  A no-op when the step had no leader-served rows
+ * (unpaired, dedup off, an end-of-ply step); a follower's spmcts_expand / spmcts_expand2 after a
+ * leader-served step without it fails (-4). */
+int spmcts_peer_push(spmcts_arena *h, float *probs_dev, float *values_dev, const float *leader_probs_dev,
+                     const float *leader_values_dev, spmcts_stream stream, spmcts_stream leader_stream);
 /* MCTreeSearch._play (mcts.py:272-299) for the active trees + remove_noise:
  * visit-count^(1/temp) distribution, np.random.choice semantics, Move record.
  * Outputs per active tree i: actions_dev[i], states_dev[i][W*H] (int8, tree

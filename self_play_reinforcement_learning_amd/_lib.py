@@ -124,6 +124,8 @@ _SIGS = {
     "spmcts_valid_moves_host": [_I32, _I32, _I32, _P, _P],
     "spmcts_table_net": [_I32, _I32, _I32, _P, _I32, _I32, _I32, _U64, _P, _P, _P, _P],
     "spmcts_set_leaf_dedup": [_P, _I32],
+    "spmcts_set_leaf_peer": [_P, _P],
+    "spmcts_peer_push": [_P, _P, _P, _P, _P, _P, _P],
     "spmcts_leaf_trees": [_P, _P, _P],
     "spmcts_copy_probe": [_P, _P, _U64, _P],
     "spmcts_conv3x3_supported": [_I32, _I32, _I32, _I32],

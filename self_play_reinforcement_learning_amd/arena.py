@@ -211,6 +211,21 @@ class Arena:
         call("spmcts_set_leaf_dedup", self.h, int(bool(on)))
         self.leaf_dedup = bool(on) and self.search_threads > 1
 
+    def set_leaf_peer(self, leader):
+        """Cross-lane leaf dedup (include/spmcts.h spmcts_set_leaf_peer): in each simulation step a pending leaf
+        whose network input `leader` (another lane's arena, stepped first) evaluates in the same step takes the
+        leader's row.  The follower's simulation-step expand is then preceded by peer_push.  None unpairs."""
+        call("spmcts_set_leaf_peer", self.h, None if leader is None else leader.h)
+        self._leader = leader  # the leader outlives the pairing (its destroy unpairs its followers)
+
+    def peer_push(self, probs, values, leader_probs, leader_values, leader_stream):
+        """Before expand() of a follower lane's simulation step: the leader's outputs of the step (its
+        evaluator's output buffers, valid on `leader_stream`) fill the leader-served rows of probs / values."""
+        assert probs.dtype == torch.float32 and probs.is_contiguous() and values.is_contiguous()
+        assert leader_probs.dtype == torch.float32 and leader_probs.is_contiguous() and leader_values.is_contiguous()
+        call("spmcts_peer_push", self.h, ptr(probs), ptr(values), ptr(leader_probs), ptr(leader_values), _stream(),
+             ctypes.c_void_p(leader_stream.cuda_stream))
+
     def set_tapes(self, tapes):
         """Parity mode: one flat float64 stream per tree (list indexed by tree id)."""
         offs = np.zeros(self.n_trees + 1, dtype=np.int64)

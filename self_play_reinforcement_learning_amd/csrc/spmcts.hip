@@ -93,6 +93,7 @@ struct View {
   int32_t *gc_list;   // [T][cap] scratch: live blocks (BFS order)
   int32_t *gc_map;    // [T][cap] scratch: old block -> new block (-1 dead)
   int32_t *tstarted;  // threaded search: search_node calls started in the current search (inactive: >= limit)
+  int32_t *tdefer;    // threaded search: 1 + the slot a deferred fill resumes at in the next launch, 0 = none
   double *noise;
   uint8_t *noise_on;
   int32_t *pnode;   // [T][MAXD] path node ids (root .. parent of leaf)
@@ -118,9 +119,16 @@ struct View {
   // one row.  dtab: open-addressing table of (generation << 32 | owner slot), dent: a slot's entry
   uint64_t *dtab;
   int32_t *dent;
-  uint8_t *down;  // 1 = the slot owns its key's row (set per step by k_dedup_owner)
+  uint8_t *down;  // 1 = the slot owns its key's row, 2 = the leader lane's row serves it (set per step)
   int dedup, dmask;
   uint32_t dgen;
+  // cross-lane dedup (round 6, spmcts_set_leaf_peer): a leader arena keeps each owner slot's key in okey
+  // (2 x u64 per slot) for the step; a follower's owner slot whose key the leader evaluates this step
+  // takes the leader's row (down 2, xpeer = the leader's owner slot), copied in by k_peer_push
+  uint64_t *okey;
+  int32_t *xpeer;
+  int lead;     // 1: this arena has followers (k_dedup_owner writes okey)
+  int peer_on;  // 1 in a follower's simulation-step launches (k_scan_need numbers down-2 slots after its own rows)
   float *root_prior;
   uint32_t *err;
   // games
@@ -335,6 +343,7 @@ __device__ __forceinline__ void reset_tree(const View &v, int tree, int player, 
   v.rplayer[tree] = (int8_t)player;
   v.noise_on[tree] = 0;
   v.tstarted[tree] = 0x3fffffff;  // no search in progress
+  v.tdefer[tree] = 0;
   for (int j = 0; j < v.K; ++j) v.need[(size_t)tree * v.K + j] = 0;
 }
 
@@ -382,6 +391,7 @@ __device__ void draw_noise(const View &v, int tree) {
   for (int j = 0; j < G::A; ++j) v.noise[(size_t)tree * G::APAD + j] = g[j];
   v.noise_on[tree] = 1;
   v.tstarted[tree] = 0;  // a search begins: `iterations` search_node calls to start
+  v.tdefer[tree] = 0;
 }
 
 // ----------------------------------------------------------------------------
@@ -1226,6 +1236,43 @@ __device__ int fill_slot_vl(const View &v, int tree, int j, int limit, int &star
   return SIM_DONE;
 }
 
+// Fill the tree's free slots from slot j0 on, each until a sim waits for the network or the search's budget
+// is spent (fill_slot_vl).  While NO slot of the tree is pending, a launch runs at most kDeferSims sims and
+// then stops; the fill resumes at the same slot in the tree's next k_expand_vl (v.tdefer).  Nothing can
+// happen in the tree in between (no pending leaf to back up, one wave owns the tree), so the tree sees
+// the same sims in the same order with the same draws: a decided endgame whose every sim ends at a
+// terminal leaf no longer runs all its sims in the ply's first select launch, which the whole chip waits
+// for, but spread over the following steps' expand launches beside the towers.
+// Completion: a deferred launch starts kDeferSims >= K sims and any other launch at least K, so a search
+// of `iterations` sims still ends within the ceil(iterations / K) network steps of the ply (k_search_end
+// checks).  Returns 1 + the slot to resume at (deferred), 0 (done or all slots pending), -1 (SIM_ERROR).
+constexpr int kDeferSims = 16;
+
+template <class G, int S>
+__device__ int fill_tree_vl(const View &v, int tree, int j0, int kt, int limit, int &started, TreeRoot &R,
+                            TreeRng &rng, bool &terr, const PathLds &pl, bool noise, double nz, SimCnt &sc,
+                            BlockCache<G::APAD, S> &bc) {
+  static_assert(kDeferSims >= 16, "a deferred launch must start at least K (<= the lane group: 8 / 16) sims");
+  int pend = 0;
+  for (int j = 0; j < kt; ++j) pend += v.need[tree * v.K + j] ? 1 : 0;
+  int ran = 0;
+  for (int j = j0; j < kt; ++j) {
+    if (v.need[tree * v.K + j]) continue;
+    while (started < limit) {
+      if (pend == 0 && ran >= kDeferSims) return j + 1;
+      ++started;
+      ++ran;
+      const int r = sim_vl<G, S>(v, tree, j, R, rng, terr, pl, noise, nz, sc, bc);
+      if (r == SIM_ERROR) return -1;
+      if (r == SIM_PENDING) {
+        ++pend;
+        break;
+      }
+    }
+  }
+  return 0;
+}
+
 // LDS block copies per tree: none in the shipped kernels.  Measured (profiles/r05/tree2/): with 16
 // copies per tree the isolated expand ran 250 -> 295-300 us and select unchanged (a launch starts with no
 // copies, so most blocks are copied once and read once; and the levels of a sim are a chain of short
@@ -1268,13 +1315,11 @@ __global__ __launch_bounds__(TB) void k_select_vl(View v, int n_active) {
   sc.prof_begin();
 #endif
   const int kt = v.tK[tree];  // this tree's sims in flight (its own thread_count, <= K)
-  for (int j = 0; j < kt; ++j) {
-    if (v.need[tree * v.K + j]) continue;
-    // SIM_ERROR (a corrupt tree: the sticky SPMCTS_ERR_STATE flag is set) ends the tree's launch; the counters
-    // of the sims completed before it are still flushed below (the failing sim's path vl is not written)
-    if (fill_slot_vl<G, S>(v, tree, j, limit, started, R, rng, terr, pl, noise, nz, sc, bc) == SIM_ERROR) break;
-  }
+  // (SIM_ERROR -- a corrupt tree: the sticky SPMCTS_ERR_STATE flag is set -- ends the tree's launch; the counters
+  // of the sims completed before it are still flushed below, the failing sim's path vl is not written)
+  const int dfr = fill_tree_vl<G, S>(v, tree, 0, kt, limit, started, R, rng, terr, pl, noise, nz, sc, bc);
   if (lane == 0) {
+    v.tdefer[tree] = dfr > 0 ? dfr : 0;
 #ifdef SPMCTS_TREE_PROF
     sc.prof_flush(0);
 #endif
@@ -1349,14 +1394,68 @@ __global__ __launch_bounds__(256) void k_dedup_insert(View v) {
 }
 
 // owner flags, one independent load pair per slot (the scan below then reads one byte per slot
-// instead of a dependent dent -> dtab chain per slot in its serial chunk loop)
+// instead of a dependent dent -> dtab chain per slot in its serial chunk loop); a leader lane also
+// keeps each owner's key for its followers' lookups this step (okey: nothing else writes it until its
+// next step's k_dedup_owner, which runs after every follower's lookup of this step)
+template <class G>
 __global__ __launch_bounds__(256) void k_dedup_owner(View v) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= v.NS) return;
-  v.down[t] = v.need[t] && (int)(uint32_t)v.dtab[v.dent[t]] == t ? 1 : 0;
+  const bool own = v.need[t] && (int)(uint32_t)v.dtab[v.dent[t]] == t;
+  v.down[t] = own ? 1 : 0;
+  if (own && v.lead) {
+    uint64_t a, b;
+    leaf_key<G>(v, t, a, b);
+    v.okey[2 * (size_t)t] = a;
+    v.okey[2 * (size_t)t + 1] = b;
+  }
 }
 
-__device__ __forceinline__ bool row_owner(const View &v, int t) { return v.dedup ? v.down[t] != 0 : v.need[t] != 0; }
+// Follower lane (spmcts_set_leaf_peer), a simulation step: owner flags as k_dedup_owner, and each owner
+// slot's key looked up in the leader lane's table of the same step (generation pgen, probed as the
+// leader's k_dedup_insert placed it: a key present this generation sits before the first entry of an
+// older one).  A hit takes the leader's row: down 2, xpeer = the leader's owner slot.  Outputs are pure
+// functions of the leaf planes (the fused trunk is batch-independent), so the leaf still gets exactly
+// the outputs its own row would have produced.
+template <class G>
+__global__ __launch_bounds__(256) void k_dedup_owner_peer(View v, const uint64_t *ptab, const uint64_t *pkey,
+                                                          int pmask, uint32_t pgen) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= v.NS) return;
+  int d = 0, xp = -1;
+  if (v.need[t] && (int)(uint32_t)v.dtab[v.dent[t]] == t) {
+    d = 1;
+    uint64_t own, opp;
+    leaf_key<G>(v, t, own, opp);
+    uint32_t h = leaf_hash(own, opp) & (uint32_t)pmask;
+    for (int probe = 0; probe <= pmask; ++probe) {
+      const unsigned long long w = ptab[h];
+      if ((uint32_t)(w >> 32) != pgen) break;  // not in the leader's batch
+      const int s = (int)(uint32_t)w;
+      if (pkey[2 * (size_t)s] == own && pkey[2 * (size_t)s + 1] == opp) {
+        d = 2;
+        xp = s;
+        break;
+      }
+      h = (h + 1) & (uint32_t)pmask;
+    }
+  }
+  v.down[t] = (uint8_t)d;
+  v.xpeer[t] = xp;
+}
+
+// the leader's outputs of this step into the follower's rows of the slots it serves (down 2), on the
+// leader's stream after its heads (spmcts_peer_push): probs [row][A] f32, values [row] f32
+__global__ __launch_bounds__(256) void k_peer_push(View v, const int32_t *psrow, const float *pprobs,
+                                                   const float *pvalues, float *probs, float *values) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= v.NS || v.down[t] != 2) return;
+  const int r1 = v.srow[t], r0 = psrow[v.xpeer[t]];
+  for (int a = 0; a < v.A; ++a) probs[(size_t)r1 * v.A + a] = pprobs[(size_t)r0 * v.A + a];
+  values[r1] = pvalues[r0];
+}
+
+__device__ __forceinline__ bool row_owner(const View &v, int t) { return v.dedup ? v.down[t] == 1 : v.need[t] != 0; }
 
 // duplicates read their owner's row
 __global__ __launch_bounds__(256) void k_dedup_alias(View v) {
@@ -1377,59 +1476,88 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_need(View v, int32_t *cou
   // wave totals of the two segments' owner counts (a two-level scan: 6 shuffle steps within each wave,
   // 3 over the 8 wave totals, 2 barriers; the round-3 1,024-entry Hillis-Steele scan took 20 barriers
   // and 8 KB of LDS)
-  __shared__ int32_t s_w0[SCAN_WAVES], s_w1[SCAN_WAVES];
+  __shared__ int32_t s_w0[SCAN_WAVES], s_w1[SCAN_WAVES], s_w2[SCAN_WAVES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T = v.NS;  // pending slots (tree * K + j), tree order then in-flight order
   const int chunk = (T + SCAN_THREADS - 1) / SCAN_THREADS;
   const int lo = min(T, tid * chunk), hi = min(T, lo + chunk);
-  int c0 = 0, c1 = 0;
+  int c0 = 0, c1 = 0, c2 = 0;
   // unrolled so each thread's chunk of flags is fetched in one round of independent loads
+  if (v.peer_on) {  // a follower's simulation step (single network): own rows, then the leader-served rows
 #pragma unroll 16
-  for (int t = lo; t < hi; ++t)
-    if (row_owner(v, t)) {
-      if (v.tnet[t / v.K]) ++c1; else ++c0;
+    for (int t = lo; t < hi; ++t) {
+      const int d = v.down[t];
+      c0 += d == 1;
+      c2 += d == 2;
     }
-  // inclusive scans of (c0, c1) in thread order: within the wave, then over the wave totals
-  int i0 = c0, i1 = c1;
+  } else {
+#pragma unroll 16
+    for (int t = lo; t < hi; ++t)
+      if (row_owner(v, t)) {
+        if (v.tnet[t / v.K]) ++c1; else ++c0;
+      }
+  }
+  // inclusive scans of (c0, c1, c2) in thread order: within the wave, then over the wave totals
+  int i0 = c0, i1 = c1, i2 = c2;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
-    const int a0 = __shfl_up(i0, off, 64), a1 = __shfl_up(i1, off, 64);
+    const int a0 = __shfl_up(i0, off, 64), a1 = __shfl_up(i1, off, 64), a2 = __shfl_up(i2, off, 64);
     if (lane >= off) {
       i0 += a0;
       i1 += a1;
+      i2 += a2;
     }
   }
   if (lane == 63) {
     s_w0[wave] = i0;
     s_w1[wave] = i1;
+    s_w2[wave] = i2;
   }
   __syncthreads();
   if (wave == 0) {
     int w0 = lane < SCAN_WAVES ? s_w0[lane] : 0, w1 = lane < SCAN_WAVES ? s_w1[lane] : 0;
+    int w2 = lane < SCAN_WAVES ? s_w2[lane] : 0;
 #pragma unroll
     for (int off = 1; off < SCAN_WAVES; off <<= 1) {
-      const int a0 = __shfl_up(w0, off, 64), a1 = __shfl_up(w1, off, 64);
+      const int a0 = __shfl_up(w0, off, 64), a1 = __shfl_up(w1, off, 64), a2 = __shfl_up(w2, off, 64);
       if (lane >= off) {
         w0 += a0;
         w1 += a1;
+        w2 += a2;
       }
     }
     if (lane < SCAN_WAVES) {
       s_w0[lane] = w0;
       s_w1[lane] = w1;
+      s_w2[lane] = w2;
     }
   }
   __syncthreads();
   i0 += wave ? s_w0[wave - 1] : 0;
   i1 += wave ? s_w1[wave - 1] : 0;
+  i2 += wave ? s_w2[wave - 1] : 0;
   int r0 = i0 - c0, r1 = v.seg1 + i1 - c1;
+  if (v.peer_on) {
+    int r2 = s_w0[SCAN_WAVES - 1] + i2 - c2;  // the leader-served rows follow all own rows
 #pragma unroll 16
-  for (int t = lo; t < hi; ++t)
-    if (row_owner(v, t)) {
-      const int r = v.tnet[t / v.K] ? r1++ : r0++;
-      v.row_tree[r] = t;
-      if (v.K > 1) v.srow[t] = r;
+    for (int t = lo; t < hi; ++t) {
+      const int d = v.down[t];
+      if (d == 1) {
+        v.row_tree[r0] = t;
+        v.srow[t] = r0++;
+      } else if (d == 2) {
+        v.srow[t] = r2++;
+      }
     }
+  } else {
+#pragma unroll 16
+    for (int t = lo; t < hi; ++t)
+      if (row_owner(v, t)) {
+        const int r = v.tnet[t / v.K] ? r1++ : r0++;
+        v.row_tree[r] = t;
+        if (v.K > 1) v.srow[t] = r;
+      }
+  }
   if (tid == SCAN_THREADS - 1) {  // the last thread's inclusive prefix is each segment's total
     v.row_count[0] = i0;
     v.row_count[1] = i1;
@@ -1616,7 +1744,29 @@ __device__ __forceinline__ void expand_vl_body(View v, const float *probs0, cons
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) s_pnode[grp][j][lane] = pn[j];
   }
-  if (!group_or<P>(my_need)) return;
+  if (!group_or<P>(my_need)) {
+    const int dfr = v.tdefer[tree];
+    if (dfr > 0) {  // a deferred fill (fill_tree_vl): resume it at its slot, nothing to back up
+      const int limit = min(v.budget[tree], v.iters);
+      int started = v.tstarted[tree];
+      const bool noise = v.noise_on[tree] != 0;
+      const double nz = (noise && lane < G::A) ? v.noise[(size_t)tree * P + lane] : 0.0;
+      TreeRng rng;
+      rng_load(v, tree, rng);
+      TreeRoot R = load_root<G>(v, tree);
+      bool terr = false;
+      SimCnt sc;
+      const int d2 = fill_tree_vl<G, S>(v, tree, dfr - 1, v.tK[tree], limit, started, R, rng, terr, pl, noise, nz, sc, bc);
+      if (lane == 0) {
+        v.tdefer[tree] = d2 > 0 ? d2 : 0;
+        sc.flush(v.cnt + (size_t)tree * C_NCNT);
+        v.tstarted[tree] = started;
+        if (terr) set_err(v, SPMCTS_ERR_TAPE);
+        rng_store(v, tree, rng);
+      }
+    }
+    return;
+  }
   const int limit = min(v.budget[tree], v.iters);
   int started = v.tstarted[tree];
   const bool refill = started < limit;
@@ -1841,6 +1991,7 @@ __device__ __forceinline__ double kahan_sum(const double *p, int n) {
 template <class G>
 __device__ PlayOut play_move_choice(const View &v, int tree, double temp, float *probs_out) {
   constexpr int P = G::APAD;
+  if (v.tdefer[tree]) set_err(v, SPMCTS_ERR_STATE);  // a deferred fill left sims unstarted (cannot happen: fill_tree_vl)
   const size_t nb = nbase<G>(v, tree);
   const int root = v.root[tree];
   const int cb = nd_c<P>(v, nb + root);
@@ -2327,6 +2478,13 @@ struct spmcts_arena {
   std::vector<void *> allocs;
   int n_active;  // active-set size for select / search_end
   int tree_block;  // threads per workgroup of the threaded tree kernels: 64 (64/P trees per wave) or P (one)
+  // cross-lane dedup (spmcts_set_leaf_peer): a follower's leader, a leader's followers, and the events that
+  // order the two streams (leader: ev_ins after its table of a step; follower: ev_rows after its rows,
+  // ev_push after the leader's outputs reached its rows)
+  spmcts_arena *peer = nullptr;
+  std::vector<spmcts_arena *> followers;
+  hipEvent_t ev_ins = nullptr, ev_rows = nullptr, ev_push = nullptr;
+  bool peer_step = false;  // the last launch_rows of this follower used the leader's table
 };
 
 static int geometry(const spmcts_config *c, int *A, int *P, int *cells, int *maxd, int *maxm) {
@@ -2382,6 +2540,7 @@ static void plan_arena(spmcts_arena *h, Plan &pl) {
   pl.add(&v.gc_list, v.gc ? T * cap : 1);
   pl.add(&v.gc_map, v.gc ? T * cap : 1);
   pl.add(&v.tstarted, T);
+  pl.add(&v.tdefer, T);
   pl.add(&v.noise, T * P);
   pl.add(&v.noise_on, T);
   const size_t NS = v.NS;  // pending slots
@@ -2411,6 +2570,8 @@ static void plan_arena(spmcts_arena *h, Plan &pl) {
     pl.add(&v.dtab, v.K > 1 ? tab : 1);
     pl.add(&v.dent, v.K > 1 ? NS : 1);
     pl.add(&v.down, v.K > 1 ? NS : 1);
+    pl.add(&v.okey, v.K > 1 ? 2 * NS : 1);
+    pl.add(&v.xpeer, v.K > 1 ? NS : 1);
   }
   pl.add(&v.root_prior, 32);  // [net][16]
   pl.add(&v.err, 4);
@@ -2497,6 +2658,7 @@ __global__ void k_rng_init(View v, uint64_t seed, uint64_t sub0) {
   ((int64_t *)v.tape_end)[t] = 0;
   for (int j = 0; j < v.K; ++j) v.need[(size_t)t * v.K + j] = 0;
   v.tstarted[t] = 0x3fffffff;
+  v.tdefer[t] = 0;
   v.noise_on[t] = 0;
   v.tnet[t] = 0;
   v.tkind[t] = SPMCTS_PLAYER_MCTS;
@@ -2639,8 +2801,55 @@ int spmcts_arena_destroy(spmcts_arena *h) {
   if (!h) return 0;
   (void)hipSetDevice(h->device);
   (void)hipDeviceSynchronize();
+  (void)spmcts_set_leaf_peer(h, nullptr);
+  for (spmcts_arena *f : h->followers) {  // a destroyed leader leaves its followers lane-local
+    f->peer = nullptr;
+    f->peer_step = false;
+  }
+  for (hipEvent_t e : {h->ev_ins, h->ev_rows, h->ev_push})
+    if (e) (void)hipEventDestroy(e);
   for (void *p : h->allocs) (void)hipFree(p);
   delete h;
+  return 0;
+}
+
+int spmcts_set_leaf_peer(spmcts_arena *h, spmcts_arena *leader) {
+  if (!h) return fail(-1, "null arena");
+  if (h->peer) {
+    auto &f = h->peer->followers;
+    f.erase(std::remove(f.begin(), f.end(), h), f.end());
+    h->peer = nullptr;
+  }
+  h->peer_step = false;
+  if (!leader) return 0;
+  if (leader == h) return fail(-3, "an arena cannot be its own leader");
+  if (leader->peer || !h->followers.empty()) return fail(-3, "one level of lanes: a leader cannot follow");
+  if (leader->cfg.game != h->cfg.game || leader->device != h->device)
+    return fail(-3, "leader and follower must play the same game on the same device");
+  if (h->v.K < 2 || leader->v.K != h->v.K) return fail(-3, "cross-lane dedup needs equal search_threads > 1");
+  if (h->v.seg1 < h->v.NS || leader->v.seg1 < leader->v.NS) return fail(-3, "cross-lane dedup: single-network arenas");
+  for (hipEvent_t *e : {&leader->ev_ins, &h->ev_rows, &h->ev_push})
+    if (!*e) HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  leader->followers.push_back(h);
+  h->peer = leader;
+  return 0;
+}
+
+int spmcts_peer_push(spmcts_arena *h, float *probs_dev, float *values_dev, const float *leader_probs_dev,
+                     const float *leader_values_dev, spmcts_stream stream, spmcts_stream leader_stream) {
+  if (!h) return fail(-1, "null arena");
+  if (!h->peer_step) return 0;
+  if (!probs_dev || !values_dev || !leader_probs_dev || !leader_values_dev) return fail(-1, "null argument");
+  const hipStream_t s = (hipStream_t)stream, ls = (hipStream_t)leader_stream;
+  // on the leader's stream, after its heads of this step: its outputs into our leader-served rows (once our
+  // rows are numbered), before it runs anything that rewrites them (its next step's heads, table or keys)
+  HIP_TRY(hipStreamWaitEvent(ls, h->ev_rows, 0));
+  hipLaunchKernelGGL(k_peer_push, dim3(nblk(h->v.NS, 256)), dim3(256), 0, ls, h->v, h->peer->v.srow, leader_probs_dev,
+                     leader_values_dev, probs_dev, values_dev);
+  HIP_TRY(hipEventRecord(h->ev_push, ls));
+  HIP_TRY(hipStreamWaitEvent(s, h->ev_push, 0));
+  h->peer_step = false;
+  LAUNCH_CHECK();
   return 0;
 }
 
@@ -2695,17 +2904,43 @@ int spmcts_search_begin(spmcts_arena *h, const int32_t *trees_dev, int32_t n, sp
   return 0;
 }
 
-static int launch_rows(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_dev, hipStream_t s) {
-  if (h->v.dedup) {
+// cross-lane dedup is live for this step: a follower whose leader and itself dedup (spmcts_set_leaf_peer)
+static bool peer_live(const spmcts_arena *h) { return h->peer && h->v.dedup && h->peer->v.dedup; }
+
+// `sim_step`: a simulation step's rows (spmcts_select / spmcts_leaf_rows), where a follower lane looks its
+// owner keys up in its leader's table; the end-of-ply expansions (spmcts_play_action, games_end_ply) stay
+// lane-local
+static int launch_rows(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_dev, hipStream_t s, bool sim_step) {
+  h->peer_step = false;
+  View v = h->v;
+  v.peer_on = 0;
+  if (v.dedup) {
     if (++h->v.dgen == 0) ++h->v.dgen;  // generation 0 = the zeroed table
-    DISPATCH(h, hipLaunchKernelGGL(k_dedup_insert<GG>, dim3(nblk(h->v.NS, 256)), dim3(256), 0, s, h->v));
-    hipLaunchKernelGGL(k_dedup_owner, dim3(nblk(h->v.NS, 256)), dim3(256), 0, s, h->v);
+    v.dgen = h->v.dgen;
+    v.lead = h->followers.empty() ? 0 : 1;
+    DISPATCH(h, hipLaunchKernelGGL(k_dedup_insert<GG>, dim3(nblk(v.NS, 256)), dim3(256), 0, s, v));
+    if (sim_step && peer_live(h)) {
+      // the leader's table and keys of this step are complete (its ev_ins), and stay so until this step's
+      // rows are numbered (the leader's stream waits for our ev_rows before it moves on: spmcts_peer_push)
+      const spmcts_arena *p = h->peer;
+      HIP_TRY(hipStreamWaitEvent(s, p->ev_ins, 0));
+      v.peer_on = 1;
+      DISPATCH(h, hipLaunchKernelGGL(k_dedup_owner_peer<GG>, dim3(nblk(v.NS, 256)), dim3(256), 0, s, v,
+                                     p->v.dtab, p->v.okey, p->v.dmask, p->v.dgen));
+    } else {
+      DISPATCH(h, hipLaunchKernelGGL(k_dedup_owner<GG>, dim3(nblk(v.NS, 256)), dim3(256), 0, s, v));
+    }
+    if (v.lead) HIP_TRY(hipEventRecord(h->ev_ins, s));
   }
-  hipLaunchKernelGGL(k_scan_need, dim3(1), dim3(SCAN_THREADS), 0, s, h->v, leaf_count_dev);
-  if (h->v.dedup) hipLaunchKernelGGL(k_dedup_alias, dim3(nblk(h->v.NS, 256)), dim3(256), 0, s, h->v);
+  hipLaunchKernelGGL(k_scan_need, dim3(1), dim3(SCAN_THREADS), 0, s, v, leaf_count_dev);
+  if (v.dedup) hipLaunchKernelGGL(k_dedup_alias, dim3(nblk(v.NS, 256)), dim3(256), 0, s, v);
+  if (v.peer_on) {
+    HIP_TRY(hipEventRecord(h->ev_rows, s));
+    h->peer_step = true;  // spmcts_peer_push brings the leader's outputs before the expand
+  }
   if (leaves_dev) {
-    const long long total = (long long)h->v.NS * h->cells;
-    DISPATCH(h, hipLaunchKernelGGL(k_encode<GG>, dim3(nblk(total, 256)), dim3(256), 0, s, h->v, leaves_dev));
+    const long long total = (long long)v.NS * h->cells;
+    DISPATCH(h, hipLaunchKernelGGL(k_encode<GG>, dim3(nblk(total, 256)), dim3(256), 0, s, v, leaves_dev));
   }
   LAUNCH_CHECK();
   return 0;
@@ -2758,7 +2993,7 @@ int spmcts_select_tree(spmcts_arena *h, spmcts_stream stream) {
 
 int spmcts_leaf_rows(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_dev, spmcts_stream stream) {
   if (!h) return fail(-1, "null arena");
-  return launch_rows(h, leaves_dev, leaf_count_dev, (hipStream_t)stream);
+  return launch_rows(h, leaves_dev, leaf_count_dev, (hipStream_t)stream, true);
 }
 
 int spmcts_select(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_dev, spmcts_stream stream) {
@@ -2770,6 +3005,7 @@ int spmcts_select(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_dev, sp
 int spmcts_expand2(spmcts_arena *h, const float *probs0_dev, const float *values0_dev, const float *probs1_dev,
                    const float *values1_dev, spmcts_stream stream) {
   if (!h) return fail(-1, "null arena");
+  if (h->peer_step) return fail(-4, "a follower lane's simulation step needs spmcts_peer_push before its expand");
   if (h->v.seg1 < h->v.NS && (!probs1_dev || !values1_dev))
     return fail(-1, "two-network arena needs network-1 outputs");
   const int gpb = 64 / h->P;
@@ -2903,7 +3139,7 @@ int spmcts_play_action(spmcts_arena *h, const int32_t *trees_dev, const int32_t 
     DISPATCH(h, hipLaunchKernelGGL(k_play_action<GG>, dim3(nblk(n, 64)), dim3(64), 0, s, h->v, trees_dev,
                                    actions_dev, n));
   LAUNCH_CHECK();
-  return launch_rows(h, leaves_dev, leaf_count_dev, s);
+  return launch_rows(h, leaves_dev, leaf_count_dev, s, false);
 }
 
 int spmcts_leaf_trees(spmcts_arena *h, int32_t *trees_dev, spmcts_stream stream) {
@@ -2988,7 +3224,7 @@ int spmcts_games_end_ply(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_
   hipStream_t s = (hipStream_t)stream;
   DISPATCH(h, hipLaunchKernelGGL(k_games_end_ply<GG>, dim3(nblk(h->v.G, 64)), dim3(64), 0, s, h->v));
   LAUNCH_CHECK();
-  return launch_rows(h, leaves_dev, leaf_count_dev, s);
+  return launch_rows(h, leaves_dev, leaf_count_dev, s, false);
 }
 
 int spmcts_games_finish_ply(spmcts_arena *h, int32_t refill, int32_t *out_dev, spmcts_stream stream) {

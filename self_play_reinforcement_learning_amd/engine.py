@@ -248,10 +248,16 @@ class SelfPlayEngine:
     def _dummy_out(self):
         return torch.zeros((1, self.arena.A), dtype=torch.float32, device=self.arena.device)
 
-    def _eval_expand_dev(self, cap=None):
+    def _eval_expand_dev(self, cap=None, sim=False):
         """Network + expand on the device-side row count: no host synchronisation.  `cap` bounds the
         rows (and so the grid): a search step has at most one leaf per game, the end-of-ply
-        expansions up to two."""
+        expansions up to two.  `sim`: a simulation step, where a follower lane (LanedEngine cross-lane
+        dedup) takes the rows its leader evaluated (Arena.peer_push)."""
+        self._eval_dev(cap)
+        self._expand_dev(sim)
+
+    def _eval_dev(self, cap=None):
+        """The network half of _eval_expand_dev (outputs kept for _expand_dev)."""
         a = self.arena
         if self.nn_timer is not None:
             self.nn_timer.start()
@@ -264,6 +270,26 @@ class SelfPlayEngine:
             p1, v1 = self.evaluator1.forward_dev(a.leaves_from(a.seg1, cap1), a.segment_count_dev(1), cap1)
         if self.nn_timer is not None:
             self.nn_timer.stop()
+        self._out = (probs, values) if self.evaluator1 is None else (probs, values, p1, v1)
+
+    def _peer_push(self, sim=True):
+        """A follower lane's simulation step: the leader's rows into ours (on the leader's stream, right after its
+        heads when LanedEngine issues every lane's network before any expand), outside the expand timer."""
+        leader = getattr(self, "_leader", None)
+        if leader is not None and sim and not getattr(self, "_pushed", False):
+            _, lp, lv = leader.evaluator._dev_bufs
+            self.arena.peer_push(self._out[0], self._out[1], lp, lv, self._leader_stream)
+            self._pushed = True
+
+    def _expand_dev(self, sim=False):
+        """The expand half of _eval_expand_dev."""
+        a = self.arena
+        self._peer_push(sim)
+        self._pushed = False
+        if self.evaluator1 is None:
+            probs, values = self._out
+        else:
+            probs, values, p1, v1 = self._out
         if self.expand_timer is not None:
             self.expand_timer.start()
         if self.evaluator1 is None:
@@ -284,11 +310,16 @@ class SelfPlayEngine:
         sims in flight only the first step launches the select kernel (it fills the K slots); later
         steps' selects run inside the expand kernel, which refills each slot right after its backup
         (the rolling schedule, csrc/spmcts.hip), so they only gather the pending leaves into rows."""
+        self._ply_sim_net(step)
+        self._expand_dev(sim=True)
+
+    def _ply_sim_net(self, step=0):
+        """The rows and network half of _ply_simulation."""
         if step == 0 or self.search_threads == 1:
             self.arena.select_async(self.select_timer)
         else:
             self.arena.leaf_rows_async()
-        self._eval_expand_dev(cap=self.n_games * self.search_threads)
+        self._eval_dev(cap=self.n_games * self.search_threads)
 
     def _ply_move(self):
         self.arena.games_end_ply_async()
@@ -456,7 +487,7 @@ class LanedEngine:
     GAME_ID_STRIDE = 1 << 40
 
     def __init__(self, game, network, n_games=4096, lanes=2, seed=0, subsequence0=None, device=None, pack=True,
-                 stagger=False, **kw):
+                 stagger=False, cross_dedup=None, **kw):
         if lanes < 1 or n_games < lanes:
             raise ValueError(f"need 1 <= lanes <= n_games (lanes={lanes}, n_games={n_games})")
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -489,6 +520,23 @@ class LanedEngine:
         self.n_games = n_games
         self.stagger = bool(stagger) and lanes > 1
         self._pending = False  # staggered lanes i > 0 are part-way through a ply
+        # cross-lane leaf dedup (round 6, include/spmcts.h spmcts_set_leaf_peer): lanes i > 0 follow lane 0 --
+        # a pending leaf whose network input lane 0 evaluates in the same simulation step takes lane 0's row.
+        # Needs lanes in lock step (no stagger), leaf dedup (pure, batch-independent evaluators) and
+        # single-network arenas; default on where those hold.  Results are unchanged bit for bit
+        # (tests/test_gpu_engine.py), only the rows evaluated drop.
+        e0 = self.lanes[0]
+        ok = (lanes > 1 and not self.stagger and e0.leaf_dedup and all(e.evaluator1 is None for e in self.lanes)
+              and all(e.arena.seg1 >= e.arena.n_trees * e.search_threads for e in self.lanes)
+              and all(e._device_count_ok() for e in self.lanes))
+        if cross_dedup and not ok:
+            raise ValueError("cross_dedup needs lanes > 1 in lock step, leaf dedup and single-network device-count "
+                             "evaluators")
+        self.cross_dedup = bool(ok if cross_dedup is None else cross_dedup)
+        if self.cross_dedup:
+            for e in self.lanes[1:]:
+                e.arena.set_leaf_peer(e0.arena)
+                e._leader, e._leader_stream = e0, self.streams[0]
         self.iterations = self.lanes[0].iterations
         self.select_steps = self.lanes[0].select_steps
         self.search_threads = self.lanes[0].search_threads
@@ -633,7 +681,12 @@ class LanedEngine:
         else:
             self._each(lambda e: e._ply_begin())
             for i in range(self.select_steps):
-                self._each(lambda e: e._ply_simulation(i))
+                # every lane's rows and network first, then the followers' leader-served rows (on lane 0's stream
+                # right after its heads, ahead of its expand), then the expands: per stream the order is one
+                # lane's ply as before
+                self._each(lambda e: e._ply_sim_net(i))
+                self._each(lambda e: e._peer_push())
+                self._each(lambda e: e._expand_dev(sim=True))
             self._each(lambda e: e._ply_move())
             res = []
             for i, (e, st) in enumerate(zip(self.lanes, self.streams)):

@@ -174,6 +174,15 @@ class _FakeLane(_FakeEngine):
     def _ply_simulation(self, step=0):
         self.sims += 1
 
+    def _ply_sim_net(self, step=0):  # LanedEngine's lock-step split of _ply_simulation
+        self.sims += 1
+
+    def _peer_push(self, sim=True):
+        pass
+
+    def _expand_dev(self, sim=False):
+        pass
+
     def _ply_move(self):
         assert self.sims == self.iterations
 

@@ -703,6 +703,77 @@ def test_leaf_dedup_is_exact(game, n_games, sims, bpt):
     assert (c1["compactions"] > 0) == (bpt > 0)  # with a small store: dedup beside subtree recycling
 
 
+@pytest.mark.parametrize("lanes,n_games,sims", [(2, 512, 16), (3, 384, 24)])
+def test_cross_lane_dedup_is_exact(lanes, n_games, sims):
+    """Cross-lane leaf dedup (LanedEngine cross_dedup, include/spmcts.h spmcts_set_leaf_peer): a follower lane's
+    leaf whose network input lane 0 evaluates in the same simulation step takes lane 0's row.  Nothing a search
+    sees changes: every lane's Move records bit for bit and the counters, with fewer network rows than
+    per-lane dedup; leaf dedup switched off mid-run (bench.py's no-dedup twin) falls back to one row per leaf
+    with the games still identical."""
+    from self_play_reinforcement_learning_amd.engine import LanedEngine
+    from self_play_reinforcement_learning_amd.modules import ResidualTower
+
+    torch.manual_seed(0)
+    net = ResidualTower(7, 6, 7, num_blocks=2, filter_factor=32).cuda().eval()
+    out = []
+    for cross in (False, True):
+        eng = LanedEngine("connect4", net, n_games=n_games, lanes=lanes, iterations=sims, seed=7, search_threads=4,
+                          max_games=4 * n_games, cross_dedup=cross)
+        assert eng.cross_dedup == cross and eng.leaf_dedup
+        got = []
+        eng.run(plies=12, on_moves=lambda m: got.append({k: v.cpu().numpy() for k, v in m.items()}))
+        eng.check()
+        c_mid = eng.counters()
+        for e in eng.lanes:  # the no-dedup twin's switch: every leaf its own row, the pairing idle
+            e.arena.set_leaf_dedup(False)
+        eng.run(plies=4, on_moves=lambda m: got.append({k: v.cpu().numpy() for k, v in m.items()}))
+        eng.check()
+        c = eng.counters()
+        assert c["nn_rows"] - c_mid["nn_rows"] == c["nn_leaves"] - c_mid["nn_leaves"]
+        out.append(({k: np.concatenate([g[k] for g in got]) for k in got[0]}, c_mid, c,
+                    [e.counters()["nn_rows"] for e in eng.lanes]))
+    (m0, c0, f0, r0), (m1, c1, f1, r1) = out
+    for k in m0:
+        np.testing.assert_array_equal(m0[k], m1[k], err_msg=k)
+    for k in ("sims", "leaked_sims", "moves", "nn_leaves", "terminal_leaves", "depth_sum", "games_finished",
+              "positions_exported", "results"):
+        assert c0[k] == c1[k] and f0[k] == f1[k], k
+    assert c1["nn_rows"] < c0["nn_rows"] < c0["nn_leaves"]
+    assert r1[0] == r0[0] and all(b < a for a, b in zip(r0[1:], r1[1:]))  # lane 0's rows unchanged
+    print(f"cross-lane dedup, {lanes} lanes: rows/leaf {c0['nn_rows'] / c0['nn_leaves']:.4f} -> "
+          f"{c1['nn_rows'] / c1['nn_leaves']:.4f}")
+
+
+def test_cross_lane_dedup_pairing_rules():
+    """spmcts_set_leaf_peer refuses pairings it cannot serve exactly (different search_threads, one-level
+    lanes only), and a follower's expand after a leader-served step without spmcts_peer_push fails loudly."""
+    from self_play_reinforcement_learning_amd import _lib
+    from self_play_reinforcement_learning_amd.arena import Arena
+
+    a = Arena("connect4", n_trees=64, iterations=8, search_threads=4, leaf_format="f32")
+    b = Arena("connect4", n_trees=64, iterations=8, search_threads=4, leaf_format="f32")
+    c = Arena("connect4", n_trees=64, iterations=8, search_threads=2, leaf_format="f32")
+    with pytest.raises(_lib.SpmctsError, match="search_threads"):
+        c.set_leaf_peer(a)
+    b.set_leaf_peer(a)
+    with pytest.raises(_lib.SpmctsError, match="leader cannot follow"):
+        a.set_leaf_peer(c)
+    for x in (a, b):
+        x.set_leaf_dedup(True)
+        x.tree_reset(list(range(64)), [1] * 64)
+        x.search_begin(list(range(64)))
+    n0 = a.select()
+    p0 = torch.full((64 * 4, 7), 1 / 7, device="cuda")
+    v0 = torch.zeros(64 * 4, device="cuda")
+    a.expand(p0[:max(n0, 1)].contiguous(), v0[:max(n0, 1)].contiguous())
+    b.select()  # every root is the same position: all of b's leaves are lane a's
+    with pytest.raises(_lib.SpmctsError, match="peer_push"):
+        b.expand(p0, v0)
+    b.set_leaf_peer(None)
+    for x in (a, b, c):
+        x.close()
+
+
 def test_leaf_dedup_two_networks_exact():
     """Evaluation arena (policy vs a second network, rows in two segments): dedup never merges rows
     of different networks, and the games come out identical."""

@@ -388,3 +388,156 @@ def test_threaded_search_vs_reference_serving_regime(pi):
     gap_ref = np.abs(sp.mean(0) - vp.mean(0))
     gap_gpu = np.abs(gp.mean(0) - vp.mean(0))
     assert (gap_gpu <= gap_ref + 4.5 * se + 2e-3).all(), (gap_ref.round(4), gap_gpu.round(4))
+
+
+# ------------------------------------------------------------------ BASELINE config 3: ResNet-256x20, 800 sims
+# No reference samples exist at this net (the reference's CPU search of ResNet-256x20 at 800 sims runs ~40 s per
+# search): the fused fp16 trunk's effect on the search is bounded against the fp32 evaluator on the SAME Philox
+# streams (same seeds, K = 4, 800 sims), the comparison the G6 shift test makes at ResNet-128x20; the bound's
+# power is shown by a half-budget control (400 sims), which must exceed it by at least 2x.  Measured
+# (profiles/r06/c256_shift.txt): the fp16 shift <= SHIFT_C256_MEASURED over the positions below.
+SHIFT_TOL_C256 = 0.003
+C256_POSITIONS = [[], [2, 4, 3, 3, 1], [3, 2, 4, 4]]  # G6 positions 0, 2, 4
+
+
+def _resnet256_evaluator(precision="fp32"):
+    """BASELINE config 3's net: ResidualTower(filter_factor=64, num_blocks=20), random init seed 0 (bench.py
+    --filter-factor 64), as the fp32 PyTorch forward or the fused HIP trunk in fp16."""
+    from self_play_reinforcement_learning_amd.evaluator import HipTowerEvaluator, TowerEvaluator
+    from self_play_reinforcement_learning_amd.modules import ResidualTower
+
+    torch.manual_seed(0)
+    net = ResidualTower(7, 6, 7, num_blocks=20, filter_factor=64).eval()
+    if precision == "fp16":
+        return HipTowerEvaluator(net.cuda(), dtype=torch.float16)
+    torch.backends.cudnn.allow_tf32 = False
+    torch.backends.cuda.matmul.allow_tf32 = False
+    return TowerEvaluator(net.cuda(), dtype=torch.float32, leaf_layout="nchw")
+
+
+_C256_FP32 = {}
+
+
+def _c256_fp32(pi, sims):
+    if (pi, sims) not in _C256_FP32:
+        _C256_FP32[(pi, sims)] = _gpu_threaded(C256_POSITIONS[pi], 2048, sims, 4, net=_resnet256_evaluator())[0]
+    return _C256_FP32[(pi, sims)]
+
+
+@pytest.mark.parametrize("pi", range(len(C256_POSITIONS)))
+def test_fused_tower_search_shift_config3(pi):
+    """Config 3's search (ResNet-256x20, 800 sims, 4 in flight, Philox): the fused fp16 trunk moves every mean
+    root visit fraction by at most SHIFT_TOL_C256 from the fp32-evaluator search on the same Philox streams."""
+    fp = _c256_fp32(pi, 800)
+    hp, _, c = _gpu_threaded(C256_POSITIONS[pi], 2048, 800, 4, net=_resnet256_evaluator("fp16"))
+    assert c["sims"] + c["leaked_sims"] == 800 * 2048
+    shift = np.abs(hp.mean(0) - fp.mean(0))
+    print(f"config3 pos {pi}: fp16 shift {shift.max():.5f} (bound {SHIFT_TOL_C256}); fp32 {fp.mean(0).round(4).tolist()}")
+    assert (shift <= SHIFT_TOL_C256).all(), (hp.mean(0).round(4), fp.mean(0).round(4))
+
+
+def test_config3_shift_check_has_power():
+    """Negative control for the bound above: the fp16 search with half the budget (400 sims) against the
+    fp32 800-sim search is rejected, by at least twice the bound at the worst position."""
+    ev = _resnet256_evaluator("fp16")
+    ex = []
+    for pi in range(len(C256_POSITIONS)):
+        fp = _c256_fp32(pi, 800)
+        hp, _, _ = _gpu_threaded(C256_POSITIONS[pi], 2048, 400, 4, net=ev)
+        ex.append(float(np.abs(hp.mean(0) - fp.mean(0)).max()))
+    print(f"config3 half-budget control: max shift per position {np.round(ex, 4).tolist()} vs bound {SHIFT_TOL_C256}")
+    assert max(ex) >= 2 * SHIFT_TOL_C256, ex
+
+
+# ------------------------------------------------------------------ BASELINE config 5: the arena's evaluate-mode search
+# G6 resnet_eval (round 6, tests/golden/run_g6_eval.sh): the reference's own threaded search with
+# MCTreeSearch.evaluate(True) -- root noise still on (mcts.py:323-327), the move drawn from n^20 (temp/20,
+# mcts.py:273-276), as both arena policies run (selfplayworker.py:71-81) -- 1,200 searches at each of 5 G6
+# positions, ResNet-128x20 seed 0, 200 sims, thread_count 4.  The arena runs it as config 5 does: the fused
+# fp16 trunk, evaluate mode, K = 4, Philox.  Both the Move's tree_probs (n^20, normalised) and the chosen-action
+# frequencies must lie within 4.5 SE + SHIFT_TOL["fp16"] of the reference's, and the mean visit fractions (the
+# reference's recorded visit counts) too.  A near-greedy choice is the mode most sensitive to a value error.
+def _eval_positions():
+    import json
+    import os
+
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "threaded_stats.json")) as f:
+        d = json.load(f)
+    return [p["pi"] for p in d["resnet_eval"]["positions"]] if "resnet_eval" in d else []
+
+
+EVAL_POSITIONS = _eval_positions()
+
+
+def _gpu_eval(opening, N, sims, K, ev, alpha=1.0):
+    """N Philox trees in an evaluate-mode arena; returns (n^20 tree_probs, actions, visit fractions)."""
+    from self_play_reinforcement_learning_amd.arena import Arena
+
+    out = {}
+    for evaluate in (True, False):  # the same seeds: the same searches; evaluate only changes _play's temp
+        arena = Arena("connect4", n_trees=N, iterations=sims, rng="philox", seed=555, leaf_format=ev.leaf_format,
+                      leaf_layout=ev.leaf_layout, search_threads=K, alpha=alpha, evaluate=evaluate)
+        root_p, _ = ev(ev.empty_root_input(7, 6, arena.device))
+        arena.set_root_prior(root_p[0])
+        arena.tree_reset(list(range(N)), [1] * N)
+
+        def step(count):
+            if count:
+                p, v = ev(arena.leaves(count))
+                arena.expand(p, v)
+
+        for a in opening:
+            step(arena.play_action(list(range(N)), [a] * N))
+        arena.search_begin(list(range(N)))
+        for _ in range(-(-sims // K)):
+            step(arena.select())
+        r = arena.search_end(1.0)
+        arena.check()
+        out[evaluate] = (r["tree_probs"].double().cpu().numpy(), r["action"].cpu().numpy())
+        arena.close()
+    return out[True][0], out[True][1], out[False][0]
+
+
+def _eval_excess(pos, gp, ga, gv):
+    """max over actions of |GPU - reference| - 4.5 SE for the n^20 tree_probs, the action frequencies and the
+    visit fractions (a value <= SHIFT_TOL passes)."""
+    cp = np.array([s["tree_probs"] for s in pos["samples"]], dtype=np.float64)
+    ca = np.array([s["action"] for s in pos["samples"]])
+    cv = np.array([s["visits"] for s in pos["samples"]], dtype=np.float64)
+    cv = cv / cv.sum(1, keepdims=True)
+    M, N = len(cp), len(gp)
+    out = []
+    for c, g in ((cp, gp), (cv, gv)):
+        se = np.sqrt(c.var(0, ddof=1) / M + g.var(0, ddof=1) / N)
+        out.append(float((np.abs(c.mean(0) - g.mean(0)) - 4.5 * se).max()))
+    fc, fg = np.bincount(ca, minlength=7) / M, np.bincount(ga, minlength=7) / N
+    sef = np.sqrt(fc * (1 - fc) / M + fg * (1 - fg) / N)
+    out.append(float((np.abs(fc - fg) - 4.5 * sef).max()))
+    return out
+
+
+@pytest.mark.skipif(not EVAL_POSITIONS, reason="G6 resnet_eval not in the fixture")
+@pytest.mark.parametrize("k", range(len(EVAL_POSITIONS)))
+def test_evaluate_mode_search_matches_reference(k):
+    d = _g6("resnet_eval")
+    pos = d["positions"][k]
+    assert pos["opening"] == [[], [3, 3, 2], [2, 4, 3, 3, 1], [3], [3, 2, 4, 4], [2, 3, 3, 4, 4, 2]][pos["pi"]]
+    assert len(pos["samples"]) >= 1000 and d["evaluate"]
+    gp, ga, gv = _gpu_eval(pos["opening"], 4096, d["sims"], d["thread_count"], _resnet_evaluator(d, "fp16"))
+    ex = _eval_excess(pos, gp, ga, gv)
+    print(f"evaluate mode pos {pos['pi']}: excess over 4.5 SE (n^20 probs, visits, actions) {np.round(ex, 4).tolist()}")
+    assert max(ex) <= SHIFT_TOL["fp16"], ex
+
+
+@pytest.mark.skipif(not EVAL_POSITIONS, reason="G6 resnet_eval not in the fixture")
+def test_evaluate_mode_check_has_power():
+    """Negative control: the same evaluate-mode comparison rejects the serial search (1 sim in flight instead
+    of the reference's thread_count) at the worst of the positions, by at least twice the bound."""
+    d = _g6("resnet_eval")
+    ev = _resnet_evaluator(d, "fp16")
+    ex = []
+    for pos in d["positions"]:
+        gp, ga, gv = _gpu_eval(pos["opening"], 4096, d["sims"], 1, ev)
+        ex.append(max(_eval_excess(pos, gp, ga, gv)))
+    print(f"evaluate mode serial control: max excess per position {np.round(ex, 4).tolist()} vs {SHIFT_TOL['fp16']}")
+    assert max(ex) >= 2 * SHIFT_TOL["fp16"], ex
