@@ -93,7 +93,6 @@ struct View {
   int32_t *gc_list;   // [T][cap] scratch: live blocks (BFS order)
   int32_t *gc_map;    // [T][cap] scratch: old block -> new block (-1 dead)
   int32_t *tstarted;  // threaded search: search_node calls started in the current search (inactive: >= limit)
-  int32_t *tdefer;    // threaded search: 1 + the slot a deferred fill resumes at in the next launch, 0 = none
   double *noise;
   uint8_t *noise_on;
   int32_t *pnode;   // [T][MAXD] path node ids (root .. parent of leaf)
@@ -343,7 +342,6 @@ __device__ __forceinline__ void reset_tree(const View &v, int tree, int player, 
   v.rplayer[tree] = (int8_t)player;
   v.noise_on[tree] = 0;
   v.tstarted[tree] = 0x3fffffff;  // no search in progress
-  v.tdefer[tree] = 0;
   for (int j = 0; j < v.K; ++j) v.need[(size_t)tree * v.K + j] = 0;
 }
 
@@ -391,7 +389,6 @@ __device__ void draw_noise(const View &v, int tree) {
   for (int j = 0; j < G::A; ++j) v.noise[(size_t)tree * G::APAD + j] = g[j];
   v.noise_on[tree] = 1;
   v.tstarted[tree] = 0;  // a search begins: `iterations` search_node calls to start
-  v.tdefer[tree] = 0;
 }
 
 // ----------------------------------------------------------------------------
@@ -1236,43 +1233,6 @@ __device__ int fill_slot_vl(const View &v, int tree, int j, int limit, int &star
   return SIM_DONE;
 }
 
-// Fill the tree's free slots from slot j0 on, each until a sim waits for the network or the search's budget
-// is spent (fill_slot_vl).  While NO slot of the tree is pending, a launch runs at most kDeferSims sims and
-// then stops; the fill resumes at the same slot in the tree's next k_expand_vl (v.tdefer).  Nothing can
-// happen in the tree in between (no pending leaf to back up, one wave owns the tree), so the tree sees
-// the same sims in the same order with the same draws: a decided endgame whose every sim ends at a
-// terminal leaf no longer runs all its sims in the ply's first select launch, which the whole chip waits
-// for, but spread over the following steps' expand launches beside the towers.
-// Completion: a deferred launch starts kDeferSims >= K sims and any other launch at least K, so a search
-// of `iterations` sims still ends within the ceil(iterations / K) network steps of the ply (k_search_end
-// checks).  Returns 1 + the slot to resume at (deferred), 0 (done or all slots pending), -1 (SIM_ERROR).
-constexpr int kDeferSims = 16;
-
-template <class G, int S>
-__device__ int fill_tree_vl(const View &v, int tree, int j0, int kt, int limit, int &started, TreeRoot &R,
-                            TreeRng &rng, bool &terr, const PathLds &pl, bool noise, double nz, SimCnt &sc,
-                            BlockCache<G::APAD, S> &bc) {
-  static_assert(kDeferSims >= 16, "a deferred launch must start at least K (<= the lane group: 8 / 16) sims");
-  int pend = 0;
-  for (int j = 0; j < kt; ++j) pend += v.need[tree * v.K + j] ? 1 : 0;
-  int ran = 0;
-  for (int j = j0; j < kt; ++j) {
-    if (v.need[tree * v.K + j]) continue;
-    while (started < limit) {
-      if (pend == 0 && ran >= kDeferSims) return j + 1;
-      ++started;
-      ++ran;
-      const int r = sim_vl<G, S>(v, tree, j, R, rng, terr, pl, noise, nz, sc, bc);
-      if (r == SIM_ERROR) return -1;
-      if (r == SIM_PENDING) {
-        ++pend;
-        break;
-      }
-    }
-  }
-  return 0;
-}
-
 // LDS block copies per tree: none in the shipped kernels.  Measured (profiles/r05/tree2/): with 16
 // copies per tree the isolated expand ran 250 -> 295-300 us and select unchanged (a launch starts with no
 // copies, so most blocks are copied once and read once; and the levels of a sim are a chain of short
@@ -1315,11 +1275,13 @@ __global__ __launch_bounds__(TB) void k_select_vl(View v, int n_active) {
   sc.prof_begin();
 #endif
   const int kt = v.tK[tree];  // this tree's sims in flight (its own thread_count, <= K)
-  // (SIM_ERROR -- a corrupt tree: the sticky SPMCTS_ERR_STATE flag is set -- ends the tree's launch; the counters
-  // of the sims completed before it are still flushed below, the failing sim's path vl is not written)
-  const int dfr = fill_tree_vl<G, S>(v, tree, 0, kt, limit, started, R, rng, terr, pl, noise, nz, sc, bc);
+  for (int j = 0; j < kt; ++j) {
+    if (v.need[tree * v.K + j]) continue;
+    // SIM_ERROR (a corrupt tree: the sticky SPMCTS_ERR_STATE flag is set) ends the tree's launch; the counters
+    // of the sims completed before it are still flushed below (the failing sim's path vl is not written)
+    if (fill_slot_vl<G, S>(v, tree, j, limit, started, R, rng, terr, pl, noise, nz, sc, bc) == SIM_ERROR) break;
+  }
   if (lane == 0) {
-    v.tdefer[tree] = dfr > 0 ? dfr : 0;
 #ifdef SPMCTS_TREE_PROF
     sc.prof_flush(0);
 #endif
@@ -1744,29 +1706,7 @@ __device__ __forceinline__ void expand_vl_body(View v, const float *probs0, cons
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) s_pnode[grp][j][lane] = pn[j];
   }
-  if (!group_or<P>(my_need)) {
-    const int dfr = v.tdefer[tree];
-    if (dfr > 0) {  // a deferred fill (fill_tree_vl): resume it at its slot, nothing to back up
-      const int limit = min(v.budget[tree], v.iters);
-      int started = v.tstarted[tree];
-      const bool noise = v.noise_on[tree] != 0;
-      const double nz = (noise && lane < G::A) ? v.noise[(size_t)tree * P + lane] : 0.0;
-      TreeRng rng;
-      rng_load(v, tree, rng);
-      TreeRoot R = load_root<G>(v, tree);
-      bool terr = false;
-      SimCnt sc;
-      const int d2 = fill_tree_vl<G, S>(v, tree, dfr - 1, v.tK[tree], limit, started, R, rng, terr, pl, noise, nz, sc, bc);
-      if (lane == 0) {
-        v.tdefer[tree] = d2 > 0 ? d2 : 0;
-        sc.flush(v.cnt + (size_t)tree * C_NCNT);
-        v.tstarted[tree] = started;
-        if (terr) set_err(v, SPMCTS_ERR_TAPE);
-        rng_store(v, tree, rng);
-      }
-    }
-    return;
-  }
+  if (!group_or<P>(my_need)) return;
   const int limit = min(v.budget[tree], v.iters);
   int started = v.tstarted[tree];
   const bool refill = started < limit;
@@ -1991,7 +1931,6 @@ __device__ __forceinline__ double kahan_sum(const double *p, int n) {
 template <class G>
 __device__ PlayOut play_move_choice(const View &v, int tree, double temp, float *probs_out) {
   constexpr int P = G::APAD;
-  if (v.tdefer[tree]) set_err(v, SPMCTS_ERR_STATE);  // a deferred fill left sims unstarted (cannot happen: fill_tree_vl)
   const size_t nb = nbase<G>(v, tree);
   const int root = v.root[tree];
   const int cb = nd_c<P>(v, nb + root);
@@ -2540,7 +2479,6 @@ static void plan_arena(spmcts_arena *h, Plan &pl) {
   pl.add(&v.gc_list, v.gc ? T * cap : 1);
   pl.add(&v.gc_map, v.gc ? T * cap : 1);
   pl.add(&v.tstarted, T);
-  pl.add(&v.tdefer, T);
   pl.add(&v.noise, T * P);
   pl.add(&v.noise_on, T);
   const size_t NS = v.NS;  // pending slots
@@ -2658,7 +2596,6 @@ __global__ void k_rng_init(View v, uint64_t seed, uint64_t sub0) {
   ((int64_t *)v.tape_end)[t] = 0;
   for (int j = 0; j < v.K; ++j) v.need[(size_t)t * v.K + j] = 0;
   v.tstarted[t] = 0x3fffffff;
-  v.tdefer[t] = 0;
   v.noise_on[t] = 0;
   v.tnet[t] = 0;
   v.tkind[t] = SPMCTS_PLAYER_MCTS;

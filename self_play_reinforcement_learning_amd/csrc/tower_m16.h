@@ -97,8 +97,7 @@ __device__ __forceinline__ void conv_tap(const char *src, const Nbr<K> &nb, f32x
 #pragma unroll
   for (int k = 0; k < KK32; ++k) {
     const int s = TAP * KK32 + k;
-    if (K::ABL & 8) {  // timing ablation (A/B library only, wrong results): no LDS operand reads
-    } else if (k + 1 < KK32) {
+    if (k + 1 < KK32) {
 #pragma unroll
       for (int t = 0; t < K::NT; ++t)
         if ((LV >> t) & 1u) {
@@ -120,8 +119,7 @@ __device__ __forceinline__ void conv_tap(const char *src, const Nbr<K> &nb, f32x
 #pragma unroll
     for (int mm = 0; mm < NM; ++mm) acur[mm] = a[slot][mm];
     const int sn = s + DEPTH;
-    if (K::ABL & 16) {  // timing ablation (A/B library only, wrong results): no weight loads in the k-loop
-    } else if (sn < STEPS) {
+    if (sn < STEPS) {
 #pragma unroll
       for (int mm = 0; mm < NM; ++mm) a[slot][mm] = wb.load(wl_off + mm * MSTRIDE + (uint32_t)sn * 1024u);
     } else if (kRingAlways || sn - STEPS < wn_steps) {
@@ -137,8 +135,6 @@ __device__ __forceinline__ void conv_tap(const char *src, const Nbr<K> &nb, f32x
           if ((LV >> t) & 1u)
             acc[mm][t][h] = mfma16<K>(acur[mm], bc[t][h], (TAP == 0 && k == 0) ? f32x4{} : acc[mm][t][h]);
     // one operand read or weight load per MFMA gap: 2 NTA LDS reads and NM weight loads among 2 NM NTA MFMAs
-    // (A/B: Cfg ABL 256 leaves the order to the compiler)
-    if constexpr (!(K::ABL & 256)) {
 #pragma unroll
     for (int i = 0; i < 2 * NTA; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
@@ -150,7 +146,6 @@ __device__ __forceinline__ void conv_tap(const char *src, const Nbr<K> &nb, f32x
       __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
     }
     __builtin_amdgcn_sched_group_barrier(0x008, 2 * NM * NTA - 2 * NTA - NM, 0);
-    }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = 0; t < K::NT; ++t) {
@@ -163,6 +158,25 @@ __device__ __forceinline__ void conv_tap(const char *src, const Nbr<K> &nb, f32x
     off_cur[t][0] = off_nxt[t][0];
     off_cur[t][1] = off_nxt[t][1];
   }
+}
+
+#ifdef SPMCTS_AB
+#include "tower_m16_abl.h"  // the k-loop's timing ablations (A/B library only)
+#endif
+
+// a tap of conv_layer: the product's conv_tap (or, in the A/B library, the ablation copy for a Cfg::ABL code)
+template <class K, int KK32, int DEPTH, int MG_, int TAP>
+__device__ __forceinline__ void tap(const char *src, const Nbr<K> &nb, f32x4 (&acc)[MM<K>][K::NT][2],
+                                    bf16x8 (&bc)[K::NT][2], bf16x8 (&bn)[K::NT][2], int (&off_cur)[K::NT][2],
+                                    int (&off_nxt)[K::NT][2], bf16x8 (&a)[DEPTH][MM<K>], int qoff, int rb,
+                                    const WBuf &wb, uint32_t wl_off, uint32_t wn_off, int wn_steps) {
+#ifdef SPMCTS_AB
+  if constexpr (K::ABL != 0) {
+    conv_tap_abl<K, KK32, DEPTH, MG_, TAP>(src, nb, acc, bc, bn, off_cur, off_nxt, a, qoff, rb, wb, wl_off, wn_off, wn_steps);
+    return;
+  }
+#endif
+  conv_tap<K, KK32, DEPTH, MG_, TAP>(src, nb, acc, bc, bn, off_cur, off_nxt, a, qoff, rb, wb, wl_off, wn_off, wn_steps);
 }
 
 // out = relu(acc + bias (+ the block input at the same physical positions, RESID)), into dst.
@@ -236,7 +250,7 @@ __device__ __forceinline__ void conv_layer(const char *src, char *dst, const Nbr
         bc[t][h] = lds_b128(src + off_cur[t][h]);
       }
     }
-#define TAP16(T) conv_tap<K, KK32, DEPTH, MG_, T>(src, nb, acc, bc, bn, off_cur, off_nxt, a, qoff, rb, wb, wl_off, wn_off, wn_steps)
+#define TAP16(T) tap<K, KK32, DEPTH, MG_, T>(src, nb, acc, bc, bn, off_cur, off_nxt, a, qoff, rb, wb, wl_off, wn_off, wn_steps)
   TAP16(0); TAP16(1); TAP16(2); TAP16(3); TAP16(4); TAP16(5); TAP16(6); TAP16(7); TAP16(8);
 #undef TAP16
   epilogue<K, RESID>(acc, dst, bv, cg, MG_, q, rb);

@@ -1,7 +1,9 @@
 // tower_wide.h — the C = 256 trunk on 6-board edge tiles with ONE activation buffer (round 3).
 //
-// Included by tower.hip (namespace tower): uses Cfg (ONEBUF), Nbr, XLive, conv_tap_x, phys_off and
-// head_layer from there.  Instantiated for the Connect4 ResNet-256 trunk (config 3: filter_factor 64).
+// Included by tower.hip (namespace tower): uses Cfg (ONEBUF), Nbr, XLive, conv_tap_x (tower_abl.h), phys_off
+// and head_layer from there.  The product's C = 256 trunk is the 16x16x32 form of this plan (tower_wide16.h),
+// which uses the residual scratch (Scr, ScrBuf) and load_bias below; the 32x32x16 k-loop, epilogue and tile
+// of this file are built into the A/B library only (SPMCTS_AB).
 //
 // Two ping-pong buffers of a 6-board tile at C = 256 would need 2 x 143.6 KB of LDS, so the two-buffer
 // kernel runs C = 256 on 3-board, board-major tiles (128 rows): no edge-tile skipping (every tap of
@@ -63,6 +65,7 @@ struct ScrBuf {
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rsrc, lane * 32 + half * 16 + so, 0, AUX);
   }
 };
+#ifdef SPMCTS_AB  // the 32x32x16 one-buffer trunk (A/B library only: SPMCTS_TOWER_C256=32, codes 23xx / 25xx)
 template <class K>
 constexpr bool kScrRsrc = (K::ABL & 2097152) == 0;
 
@@ -134,6 +137,7 @@ __device__ __forceinline__ void epilogue(char *X, const f32x16 (&acc)[K::MT][K::
   }
   __syncthreads();
 }
+#endif  // SPMCTS_AB
 
 template <class K>
 __device__ __forceinline__ void load_bias(float4 (&bv)[K::MT][4], const float *bias, int wave, int lane) {
@@ -143,6 +147,7 @@ __device__ __forceinline__ void load_bias(float4 (&bv)[K::MT][4], const float *b
     for (int g = 0; g < 4; ++g) bv[m][g] = *(const float4 *)(bias + (wave * K::MT + m) * 32 + 8 * g + 4 * (lane >> 5));
 }
 
+#ifdef SPMCTS_AB
 // One 3x3 conv over the resident tile, in place (the k-loop is conv_layer_x's edge-tile path).
 template <class K, int KK, int DEPTH, bool RESID, bool SAVE>
 __device__ __forceinline__ void conv(char *X, const Nbr<K> &nb, bf16x8 (&a)[DEPTH][K::MT], const float *bias, int wave,
@@ -288,5 +293,7 @@ __device__ __forceinline__ void tile(char *smem, const __bf16 *planes, int batch
   }
   head_layer<K>(X, wblk + (size_t)n_convs * LAYER, b, out, board0, batch, wave, lane);
 }
+
+#endif  // SPMCTS_AB
 
 }  // namespace wide
