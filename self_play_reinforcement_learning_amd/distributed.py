@@ -289,10 +289,12 @@ def check_devices(n):
 
 
 def assert_gpu_untouched(what):
-    """The parent of N rank processes must not have initialised HIP: a GPU-initialised process may
-    start children but never exec, and its own device context would sit on GPU 0 beside rank 0's for the
-    whole job.  Raises RuntimeError if it has (torch.cuda.is_initialized(): device counting does not
-    initialise, any allocation or kernel does)."""
+    """launch_script's parent (bench.py --gpus N) only waits for its N rank processes: it must not have
+    initialised HIP, or its own device context would sit on GPU 0 beside rank 0's for the whole job (and a
+    GPU-initialised process may start children but never exec).  Raises RuntimeError if it has
+    (torch.cuda.is_initialized(): device counting does not initialise, any allocation or kernel does).
+    spawn_ranks (SelfPlayScheduler(gpus=N)) does not assert this: its parent keeps the caller's network and
+    may have used the GPU before (a notebook, the GPU tests), and starting child processes from it is safe."""
     if torch.cuda.is_initialized():
         raise RuntimeError(f"{what}: this process has already initialised the GPU; start the rank processes "
                            f"before any GPU call (bench.py --gpus N and SelfPlayScheduler(gpus=N) do)")
@@ -344,7 +346,6 @@ def spawn_ranks(fn, n, *args, timeout=None, **kwargs):
     import multiprocessing as mp
     from multiprocessing.connection import wait
 
-    assert_gpu_untouched("spawn_ranks")
     ctx = mp.get_context("spawn")
     port = free_port()
     procs = [ctx.Process(target=_spawned_rank, args=(r, n, port, fn, args, kwargs)) for r in range(n)]

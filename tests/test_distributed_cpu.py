@@ -620,15 +620,12 @@ def test_scheduler_rank_count_and_spawn_kwargs(tmp_path, monkeypatch):
     assert isinstance(kw["evaluation_policy_container"].policy_kwargs["network"], ResidualTower)
 
 
-def test_launchers_refuse_a_gpu_initialised_parent(monkeypatch):
-    """launch_script / spawn_ranks start the rank processes only from a parent that has not initialised HIP
-    (bench.py --gpus N, SelfPlayScheduler(gpus=N)); with torch.cuda.is_initialized() True they raise before
-    starting anything."""
+def test_launch_script_refuses_a_gpu_initialised_parent(monkeypatch):
+    """launch_script (bench.py --gpus N) starts the rank processes only from a parent that has not initialised
+    HIP; with torch.cuda.is_initialized() True it raises before starting anything."""
     monkeypatch.setattr(torch.cuda, "is_initialized", lambda: True)
     with pytest.raises(RuntimeError, match="initialised the GPU"):
         D.launch_script(["-c", "raise SystemExit(3)"], 2)
-    with pytest.raises(RuntimeError, match="initialised the GPU"):
-        D.spawn_ranks(print, 2)
     monkeypatch.undo()
     assert not torch.cuda.is_initialized()
     assert D.launch_script(["-c", "raise SystemExit(0)"], 2) == 0
