@@ -322,6 +322,9 @@ def main():
     ap.add_argument("--no-cross-dedup", action="store_true",
                     help="lanes > 1: per-lane leaf dedup only (default: a lane-1 leaf whose input lane 0 evaluates in "
                          "the same simulation step takes lane 0's row, engine.LanedEngine cross_dedup)")
+    ap.add_argument("--lane0-share", type=float, default=None,
+                    help="lanes = 2: lane 0's share of the games (default an even split); with cross-lane dedup lane 1 "
+                         "evaluates fewer rows per game")
     ap.add_argument("--no-pack", action="store_true",
                     help="lanes > 1: keep round-aligned tower tiles (no SPMCTS_TOWER_PACK)")
     ap.add_argument("--twin-no-dedup", type=int, default=5, metavar="PLIES",
@@ -391,8 +394,13 @@ def main():
               evaluate=arena_mode, record=not arena_mode, search_threads=args.search_threads,
               blocks_per_tree=args.blocks_per_tree, leaf_dedup=False if args.no_leaf_dedup else None)
     if args.lanes > 1:
+        lane_sizes = None
+        if args.lane0_share is not None and args.lanes == 2:
+            n0 = int(round(args.games * args.lane0_share))
+            lane_sizes = [n0, args.games - n0]
         eng = LanedEngine("connect4", net, n_games=args.games, lanes=args.lanes, pack=not args.no_pack,
-                          stagger=args.stagger, cross_dedup=False if args.no_cross_dedup else None, **kw)
+                          stagger=args.stagger, cross_dedup=False if args.no_cross_dedup else None,
+                          lane_sizes=lane_sizes, **kw)
     else:
         eng = SelfPlayEngine("connect4", net, n_games=args.games, **kw)
     gathered = []
@@ -553,6 +561,7 @@ def main():
             "parallelism": f"dp{world}",
             "lanes_per_gpu": max(1, args.lanes),
             "lanes_staggered": bool(getattr(eng, "stagger", False)) if args.lanes > 1 else False,
+            "lane_games": [e.n_games for e in eng.lanes] if args.lanes > 1 else [args.games],
             "search_threads": args.search_threads,
             "leaf_dedup": bool(getattr(eng, "leaf_dedup", False)),
             "cross_lane_dedup": bool(getattr(eng, "cross_dedup", False)),

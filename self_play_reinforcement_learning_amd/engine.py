@@ -487,7 +487,7 @@ class LanedEngine:
     GAME_ID_STRIDE = 1 << 40
 
     def __init__(self, game, network, n_games=4096, lanes=2, seed=0, subsequence0=None, device=None, pack=True,
-                 stagger=False, cross_dedup=None, **kw):
+                 stagger=False, cross_dedup=None, lane_sizes=None, **kw):
         if lanes < 1 or n_games < lanes:
             raise ValueError(f"need 1 <= lanes <= n_games (lanes={lanes}, n_games={n_games})")
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -495,6 +495,10 @@ class LanedEngine:
         if subsequence0 is None:
             subsequence0 = rank * 2 * n_games
         sizes = [n_games // lanes + (1 if i < n_games % lanes else 0) for i in range(lanes)]
+        if lane_sizes is not None:  # an explicit split of the n_games slots over the lanes
+            sizes = [int(x) for x in lane_sizes]
+            if len(sizes) != lanes or sum(sizes) != n_games or min(sizes) < 1:
+                raise ValueError(f"lane_sizes {lane_sizes} must be {lanes} positive counts summing to {n_games}")
         # a game budget is split like the slots (each lane stops starting games at its share)
         self.max_games = kw.pop("max_games", None)
         budgets = [None] * lanes if self.max_games is None else \
