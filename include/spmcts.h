@@ -64,7 +64,7 @@ enum spmcts_player_kind {
 /* return code of the tower entry points (spmcts_tower_forward*, spmcts_tower_heads*) and of
  * spmcts_arena_create: an environment switch of the A/B library (SPMCTS_TOWER_CG, SPMCTS_TOWER_RING,
  * SPMCTS_TOWER_C256, SPMCTS_WIDE_TAILS, SPMCTS_HEADS, SPMCTS_HEADS_C256, SPMCTS_TREE_BLOCK,
- * SPMCTS_EXPAND_CO, SPMCTS_TOWER_M16, SPMCTS_TREE_COPIES -- whatever its value; `make ab` builds libspmcts_ab.so, which
+ * SPMCTS_EXPAND_CO, SPMCTS_TOWER_M16, SPMCTS_TREE_COPIES, SPMCTS_PEER_PUSH -- whatever its value; `make ab` builds libspmcts_ab.so, which
  * reads them) is set while the product library is loaded: refused instead of silently ignored */
 #define SPMCTS_ERR_AB_SWITCH (-5)
 

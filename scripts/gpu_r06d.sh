@@ -1,4 +1,6 @@
 # Round 6, fourth pass (the final tree):
+#  (0) the cross-lane / dedup engine tests; the peer push on the follower's push stream vs on the leader's
+#      stream (A/B library, SPMCTS_PEER_PUSH=leader), alternated;
 #  (1) lane split A/B with cross-lane dedup (lane 0's share 0.5 / 0.48 / 0.46), alternated;
 #  (2) the profile bundle of the driver's command (--warmup 5 --steps 20, same seeds; CPU leg and no-dedup twin
 #      off so the trace's last dispatches are the timed region): kernel trace + stats, trace-recomputed roofline,
@@ -12,6 +14,18 @@ export TMPDIR=/tmp
 ARGS="--steps 20 --warmup 5 --no-cpu-baseline --twin-no-dedup 0"
 val() { python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][0]); print(round(d['value']), round(d['roofline']['frac'],4), round(d['nn']['rows_per_leaf'],4), round(d['nn']['share_of_step'],4), d['config'].get('lane_games'), round(d['roofline']['clock']['clock_ghz'],3))" "$1"; }
 ndisp() { python3 -c "import json,sys; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][0]); print(d['roofline']['dispatches'])" "$1"; }
+AB=$PWD/self_play_reinforcement_learning_amd/libspmcts_ab.so
+timeout -k 10 600 python -u -m pytest tests/test_gpu_engine.py -m gpu -x -q --timeout 300 --timeout-method thread \
+  -k "cross_lane or leaf_dedup or laned" > $O/tests.log 2>&1
+rc=$?; tail -1 $O/tests.log | tee -a $O/summary.txt; [ $rc -eq 0 ] || { grep -B5 -A40 "FAILED\|Error" $O/tests.log | head -80; exit $rc; }
+for rep in 1 2; do
+  for v in stream leader; do
+    if [ $v = leader ]; then export SPMCTS_PEER_PUSH=leader; else unset SPMCTS_PEER_PUSH; fi
+    SPMCTS_LIB=$AB timeout -k 10 300 python3 bench.py $ARGS > $O/p_${v}_$rep.json 2> $O/err.txt || { tail -5 $O/err.txt; exit 1; }
+    echo "bench push on $v (A/B lib): $(val $O/p_${v}_$rep.json)" | tee -a $O/summary.txt
+  done
+done
+unset SPMCTS_PEER_PUSH
 for rep in 1 2; do
   for sh in 0.5 0.48 0.46; do
     timeout -k 10 300 python3 bench.py $ARGS --lane0-share $sh > $O/b_${sh}_$rep.json 2> $O/err.txt || { tail -5 $O/err.txt; exit 1; }

@@ -2422,8 +2422,10 @@ struct spmcts_arena {
   // ev_push after the leader's outputs reached its rows)
   spmcts_arena *peer = nullptr;
   std::vector<spmcts_arena *> followers;
-  hipEvent_t ev_ins = nullptr, ev_rows = nullptr, ev_push = nullptr;
+  hipEvent_t ev_ins = nullptr, ev_rows = nullptr, ev_push = nullptr, ev_lead = nullptr;
+  hipStream_t push_stream = nullptr;  // a follower's stream for k_peer_push (spmcts_peer_push)
   bool peer_step = false;  // the last launch_rows of this follower used the leader's table
+  bool push_pending = false;  // the leader's stream has not yet waited for this follower's last push
 };
 
 static int geometry(const spmcts_config *c, int *A, int *P, int *cells, int *maxd, int *maxm) {
@@ -2680,7 +2682,7 @@ int spmcts_arena_create(const spmcts_config *cfg, int device, spmcts_arena **out
     return rc;
   }
 #ifndef SPMCTS_AB
-  for (const char *n : {"SPMCTS_TREE_BLOCK", "SPMCTS_EXPAND_CO", "SPMCTS_TREE_COPIES"})
+  for (const char *n : {"SPMCTS_TREE_BLOCK", "SPMCTS_EXPAND_CO", "SPMCTS_TREE_COPIES", "SPMCTS_PEER_PUSH"})
     if (getenv(n)) {
       delete h;
       return fail(SPMCTS_ERR_AB_SWITCH, std::string(n) + " is a switch of the A/B library (make ab: libspmcts_ab.so)");
@@ -2743,8 +2745,9 @@ int spmcts_arena_destroy(spmcts_arena *h) {
     f->peer = nullptr;
     f->peer_step = false;
   }
-  for (hipEvent_t e : {h->ev_ins, h->ev_rows, h->ev_push})
+  for (hipEvent_t e : {h->ev_ins, h->ev_rows, h->ev_push, h->ev_lead})
     if (e) (void)hipEventDestroy(e);
+  if (h->push_stream) (void)hipStreamDestroy(h->push_stream);
   for (void *p : h->allocs) (void)hipFree(p);
   delete h;
   return 0;
@@ -2758,6 +2761,7 @@ int spmcts_set_leaf_peer(spmcts_arena *h, spmcts_arena *leader) {
     h->peer = nullptr;
   }
   h->peer_step = false;
+  h->push_pending = false;
   if (!leader) return 0;
   if (leader == h) return fail(-3, "an arena cannot be its own leader");
   if (leader->peer || !h->followers.empty()) return fail(-3, "one level of lanes: a leader cannot follow");
@@ -2765,12 +2769,23 @@ int spmcts_set_leaf_peer(spmcts_arena *h, spmcts_arena *leader) {
     return fail(-3, "leader and follower must play the same game on the same device");
   if (h->v.K < 2 || leader->v.K != h->v.K) return fail(-3, "cross-lane dedup needs equal search_threads > 1");
   if (h->v.seg1 < h->v.NS || leader->v.seg1 < leader->v.NS) return fail(-3, "cross-lane dedup: single-network arenas");
-  for (hipEvent_t *e : {&leader->ev_ins, &h->ev_rows, &h->ev_push})
+  for (hipEvent_t *e : {&leader->ev_ins, &h->ev_rows, &h->ev_push, &h->ev_lead})
     if (!*e) HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
   leader->followers.push_back(h);
   h->peer = leader;
   return 0;
 }
+
+#ifdef SPMCTS_AB
+// SPMCTS_PEER_PUSH=leader (A/B library): the push on the leader's own stream ahead of its expand (round 6's
+// first form), instead of on the follower's push stream
+static bool push_on_leader() {
+  static const bool v = getenv("SPMCTS_PEER_PUSH") && strcmp(getenv("SPMCTS_PEER_PUSH"), "leader") == 0;
+  return v;
+}
+#else
+static constexpr bool push_on_leader() { return false; }
+#endif
 
 int spmcts_peer_push(spmcts_arena *h, float *probs_dev, float *values_dev, const float *leader_probs_dev,
                      const float *leader_values_dev, spmcts_stream stream, spmcts_stream leader_stream) {
@@ -2778,12 +2793,26 @@ int spmcts_peer_push(spmcts_arena *h, float *probs_dev, float *values_dev, const
   if (!h->peer_step) return 0;
   if (!probs_dev || !values_dev || !leader_probs_dev || !leader_values_dev) return fail(-1, "null argument");
   const hipStream_t s = (hipStream_t)stream, ls = (hipStream_t)leader_stream;
-  // on the leader's stream, after its heads of this step: its outputs into our leader-served rows (once our
-  // rows are numbered), before it runs anything that rewrites them (its next step's heads, table or keys)
-  HIP_TRY(hipStreamWaitEvent(ls, h->ev_rows, 0));
-  hipLaunchKernelGGL(k_peer_push, dim3(nblk(h->v.NS, 256)), dim3(256), 0, ls, h->v, h->peer->v.srow, leader_probs_dev,
-                     leader_values_dev, probs_dev, values_dev);
-  HIP_TRY(hipEventRecord(h->ev_push, ls));
+  if (push_on_leader()) {
+    // on the leader's stream, after its heads of this step (ahead of its expand)
+    HIP_TRY(hipStreamWaitEvent(ls, h->ev_rows, 0));
+    hipLaunchKernelGGL(k_peer_push, dim3(nblk(h->v.NS, 256)), dim3(256), 0, ls, h->v, h->peer->v.srow,
+                       leader_probs_dev, leader_values_dev, probs_dev, values_dev);
+    HIP_TRY(hipEventRecord(h->ev_push, ls));
+  } else {
+    // on the follower's own push stream, once the leader's outputs of this step (everything the caller has
+    // issued on leader_stream: its heads) and our rows are there; the leader's stream goes on at once (its
+    // expand does not wait) and waits for the push only before it next rewrites its table, keys or outputs
+    // (launch_rows: its next step's rows)
+    if (!h->push_stream) HIP_TRY(hipStreamCreateWithFlags(&h->push_stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventRecord(h->ev_lead, ls));
+    HIP_TRY(hipStreamWaitEvent(h->push_stream, h->ev_lead, 0));
+    HIP_TRY(hipStreamWaitEvent(h->push_stream, h->ev_rows, 0));
+    hipLaunchKernelGGL(k_peer_push, dim3(nblk(h->v.NS, 256)), dim3(256), 0, h->push_stream, h->v, h->peer->v.srow,
+                       leader_probs_dev, leader_values_dev, probs_dev, values_dev);
+    HIP_TRY(hipEventRecord(h->ev_push, h->push_stream));
+    h->push_pending = true;
+  }
   HIP_TRY(hipStreamWaitEvent(s, h->ev_push, 0));
   h->peer_step = false;
   LAUNCH_CHECK();
@@ -2849,6 +2878,11 @@ static bool peer_live(const spmcts_arena *h) { return h->peer && h->v.dedup && h
 // lane-local
 static int launch_rows(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_dev, hipStream_t s, bool sim_step) {
   h->peer_step = false;
+  for (spmcts_arena *f : h->followers)  // a leader rewrites its table, keys and (later) outputs only after the pushes
+    if (f->push_pending) {
+      HIP_TRY(hipStreamWaitEvent(s, f->ev_push, 0));
+      f->push_pending = false;
+    }
   View v = h->v;
   v.peer_on = 0;
   if (v.dedup) {

@@ -25,7 +25,8 @@ def product_env():
     """Environment of a child process on the product library (no A/B switch set)."""
     env = {k: v for k, v in os.environ.items() if k != "SPMCTS_LIB" and not k.startswith(("SPMCTS_TOWER_", "SPMCTS_HEADS",
                                                                                             "SPMCTS_WIDE_", "SPMCTS_TREE_BLOCK",
-                                                                                            "SPMCTS_EXPAND_CO", "SPMCTS_TREE_COPIES"))}
+                                                                                            "SPMCTS_EXPAND_CO", "SPMCTS_TREE_COPIES",
+                                                                                            "SPMCTS_PEER_PUSH"))}
     return env
 
 
