@@ -273,8 +273,8 @@ class SelfPlayEngine:
         self._out = (probs, values) if self.evaluator1 is None else (probs, values, p1, v1)
 
     def _peer_push(self, sim=True):
-        """A follower lane's simulation step: the leader's rows into ours (on the leader's stream, right after its
-        heads when LanedEngine issues every lane's network before any expand), outside the expand timer."""
+        """A follower lane's simulation step: the leader's rows into ours (include/spmcts.h spmcts_peer_push: on the
+        follower's push stream, once the leader's heads and our rows are done), outside the expand timer."""
         leader = getattr(self, "_leader", None)
         if leader is not None and sim and not getattr(self, "_pushed", False):
             _, lp, lv = leader.evaluator._dev_bufs
@@ -685,9 +685,8 @@ class LanedEngine:
         else:
             self._each(lambda e: e._ply_begin())
             for i in range(self.select_steps):
-                # every lane's rows and network first, then the followers' leader-served rows (on lane 0's stream
-                # right after its heads, ahead of its expand), then the expands: per stream the order is one
-                # lane's ply as before
+                # every lane's rows and network first, then the followers' leader-served rows (issued once lane 0's
+                # heads are queued: spmcts_peer_push), then the expands; per stream the order is one lane's ply
                 self._each(lambda e: e._ply_sim_net(i))
                 self._each(lambda e: e._peer_push())
                 self._each(lambda e: e._expand_dev(sim=True))
