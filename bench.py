@@ -44,7 +44,7 @@ sys.path.insert(0, HERE)
 
 TRAFFIC_FILE = os.path.join(HERE, "profiles", "r01_bench_prof", "k_tower_traffic.json")  # --search-threads 1
 TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r06_bench_prof", "k_tower_traffic.json")  # 4 (default)
-TREE_TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r05_tree_pmc", "tree_traffic.json")
+TREE_TRAFFIC_FILE_K4 = os.path.join(HERE, "profiles", "r06_tree_pmc", "tree_traffic.json")
 # in-bench MFMA-busy share (and profiled clock) of the timed k_tower_dyn dispatches (one PMC pass per trunk dtype,
 # scripts/gpu_r06a.sh -> scripts/tower_util.py): the roofline's frac ~ busy x clock / 2.4 GHz / 0.833
 CLOCK_FILES = {"fp16": os.path.join(HERE, "profiles", "r06_bench_prof", "tower_util_bench_fp16.json"),
