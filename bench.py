@@ -129,6 +129,11 @@ class GfxClock:
         self._stop.set()
         if self._thread is not None:
             self._thread.join()
+        if self.err is None:
+            try:
+                self._smi.amdsmi_shut_down()
+            except Exception:
+                pass
 
     def report(self):
         clk = [c for c, _ in self.samples if c is not None]

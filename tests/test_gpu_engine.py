@@ -703,8 +703,11 @@ def test_leaf_dedup_is_exact(game, n_games, sims, bpt):
     assert (c1["compactions"] > 0) == (bpt > 0)  # with a small store: dedup beside subtree recycling
 
 
-@pytest.mark.parametrize("lanes,n_games,sims", [(2, 512, 16), (3, 384, 24)])
-def test_cross_lane_dedup_is_exact(lanes, n_games, sims):
+@pytest.mark.parametrize("lanes,n_games,sims,game,bpt,sizes", [(2, 512, 16, "connect4", 0, None),
+                                                                (3, 384, 24, "connect4", 0, None),
+                                                                (2, 256, 24, "tictactoe", 0, None),
+                                                                (2, 256, 16, "connect4", 6 * 16 + 64, [118, 138])])
+def test_cross_lane_dedup_is_exact(lanes, n_games, sims, game, bpt, sizes):
     """Cross-lane leaf dedup (LanedEngine cross_dedup, include/spmcts.h spmcts_set_leaf_peer): a follower lane's
     leaf whose network input lane 0 evaluates in the same simulation step takes lane 0's row.  Nothing a search
     sees changes: every lane's Move records bit for bit and the counters, with fewer network rows than
@@ -714,11 +717,13 @@ def test_cross_lane_dedup_is_exact(lanes, n_games, sims):
     from self_play_reinforcement_learning_amd.modules import ResidualTower
 
     torch.manual_seed(0)
-    net = ResidualTower(7, 6, 7, num_blocks=2, filter_factor=32).cuda().eval()
+    W, H, A = (7, 6, 7) if game == "connect4" else (3, 3, 9)
+    net = ResidualTower(W, H, A, num_blocks=2, filter_factor=32).cuda().eval()
     out = []
     for cross in (False, True):
-        eng = LanedEngine("connect4", net, n_games=n_games, lanes=lanes, iterations=sims, seed=7, search_threads=4,
-                          max_games=4 * n_games, cross_dedup=cross)
+        # (TicTacToe; a recycled node store beside the pairing; unequal lanes, as bench.py's 0.48 split)
+        eng = LanedEngine(game, net, n_games=n_games, lanes=lanes, iterations=sims, seed=7, search_threads=4,
+                          max_games=4 * n_games, cross_dedup=cross, blocks_per_tree=bpt, lane_sizes=sizes)
         assert eng.cross_dedup == cross and eng.leaf_dedup
         got = []
         eng.run(plies=12, on_moves=lambda m: got.append({k: v.cpu().numpy() for k, v in m.items()}))
@@ -740,7 +745,8 @@ def test_cross_lane_dedup_is_exact(lanes, n_games, sims):
         assert c0[k] == c1[k] and f0[k] == f1[k], k
     assert c1["nn_rows"] < c0["nn_rows"] < c0["nn_leaves"]
     assert r1[0] == r0[0] and all(b < a for a, b in zip(r0[1:], r1[1:]))  # lane 0's rows unchanged
-    print(f"cross-lane dedup, {lanes} lanes: rows/leaf {c0['nn_rows'] / c0['nn_leaves']:.4f} -> "
+    assert (c1["compactions"] > 0) == (bpt > 0)
+    print(f"cross-lane dedup, {game} {lanes} lanes: rows/leaf {c0['nn_rows'] / c0['nn_leaves']:.4f} -> "
           f"{c1['nn_rows'] / c1['nn_leaves']:.4f}")
 
 
