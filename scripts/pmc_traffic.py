@@ -23,12 +23,13 @@ def mean_counter(path, name, kernel="k_tower_dyn", last=0):
     return sum(vals) / len(vals), len(vals)
 
 
-def main(fetch_csv, write_csv, out_json, lanes="1", last="0"):
+def main(fetch_csv, write_csv, out_json, lanes="1", last="0", kernel="k_tower_dyn"):
+    """`kernel`: a substring of the kernel name (k_tower for the host-count trunk of scripts/bench_tower.py)."""
     lanes, last = int(lanes), int(last)
-    fetch, n = mean_counter(fetch_csv, "FETCH_SIZE", last=last)
-    write, _ = mean_counter(write_csv, "WRITE_SIZE", last=last)
+    fetch, n = mean_counter(fetch_csv, "FETCH_SIZE", kernel=kernel, last=last)
+    write, _ = mean_counter(write_csv, "WRITE_SIZE", kernel=kernel, last=last)
     per_dispatch = 2 * fetch * 1024 + write * 1024
-    res = dict(kernel="k_tower_dyn", dispatches=n, lanes=lanes, fetch_kib=fetch, write_kib=write,
+    res = dict(kernel=kernel, dispatches=n, lanes=lanes, fetch_kib=fetch, write_kib=write,
                read_bytes=2 * fetch * 1024, write_bytes=write * 1024,
                bytes_per_dispatch=per_dispatch,
                bytes_per_launch=per_dispatch * lanes,

@@ -1453,6 +1453,9 @@ static int forward_ab(int32_t width, int32_t height, int32_t channels, int32_t n
       // LDS operand reads (1608) -- upper bounds on what fewer weight / operand fetches per MFMA could buy
       case 1616: return launch<Cfg<128, 256, 7, 6, 2, 4, 16, 2, 1, true, true, __bf16, false, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       case 1608: return launch<Cfg<128, 256, 7, 6, 2, 4, 8, 2, 1, true, true, __bf16, false, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
+      // timing ablation (wrong results): every layer streams layer 0's weights (an L2-resident set): what the
+      // trunk's fabric re-stream of its 11.8 MB weight set costs
+      case 1665: return launch<Cfg<128, 256, 7, 6, 2, 4, 65536, 2, 1, true, true, __bf16, false, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       // timing ablation (wrong results): two 16x16x32 MFMAs per 32x32x16 (the MFMA-shape clock probe)
       case 308: return launch<Cfg<128, 256, 7, 6, 2, 4, 8388608, 4, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);
       case 302: return launch<Cfg<128, 256, 7, 6, 2, 4, 8192, 4, 1, true, true>>(pl, batch, n_blocks, weights_dev, bias_dev, ft, s);

@@ -362,8 +362,16 @@ __device__ __forceinline__ void tile(char *smem, const __bf16 *planes, int batch
   const int cg_u = __builtin_amdgcn_readfirstlane(cg);
   const uint32_t ct0_off = (uint32_t)(STEM + (size_t)(NM * cg_u) * LSTEPS * 64) * 16u;
   for (int L = 0; L < n_convs; ++L) {
+#ifdef SPMCTS_AB
+    // timing ablation (A/B code 1665, wrong results): every layer streams layer 0's weights, an L2-resident
+    // 295 KB set instead of 11.8 MB re-streamed from the fabric per round of workgroups
+    const bool l2w = (K::ABL & 65536) != 0;
+    const uint32_t wl_off = ct0_off + (l2w ? 0u : (uint32_t)((size_t)L * LAYER * 16u));
+    const uint32_t wn_off = (l2w || (kRingAlways && L + 1 == n_convs)) ? wl_off : wl_off + (uint32_t)(LAYER * 16u);
+#else
     const uint32_t wl_off = ct0_off + (uint32_t)((size_t)L * LAYER * 16u);
     const uint32_t wn_off = (kRingAlways && L + 1 == n_convs) ? wl_off : wl_off + (uint32_t)(LAYER * 16u);
+#endif
     const int wn_steps = L + 1 < n_convs ? LSTEPS : 0;
     const bool even = (L & 1) == 0;
     if (K::MG == 1 || wave / K::CG == 0) {

@@ -706,7 +706,7 @@ def test_leaf_dedup_is_exact(game, n_games, sims, bpt):
 @pytest.mark.parametrize("lanes,n_games,sims,game,bpt,sizes", [(2, 512, 16, "connect4", 0, None),
                                                                 (3, 384, 24, "connect4", 0, None),
                                                                 (2, 256, 24, "tictactoe", 0, None),
-                                                                (2, 256, 16, "connect4", 6 * 16 + 64, [118, 138])])
+                                                                (2, 256, 16, "connect4", 2 * 16 + 64, [118, 138])])
 def test_cross_lane_dedup_is_exact(lanes, n_games, sims, game, bpt, sizes):
     """Cross-lane leaf dedup (LanedEngine cross_dedup, include/spmcts.h spmcts_set_leaf_peer): a follower lane's
     leaf whose network input lane 0 evaluates in the same simulation step takes lane 0's row.  Nothing a search
@@ -721,7 +721,8 @@ def test_cross_lane_dedup_is_exact(lanes, n_games, sims, game, bpt, sizes):
     net = ResidualTower(W, H, A, num_blocks=2, filter_factor=32).cuda().eval()
     out = []
     for cross in (False, True):
-        # (TicTacToe; a recycled node store beside the pairing; unequal lanes, as bench.py's 0.48 split)
+        # (TicTacToe; a recycled node store beside the pairing -- 96 blocks per tree: compacted within the 12
+        # plies --; unequal lanes, as bench.py's 0.48 split)
         eng = LanedEngine(game, net, n_games=n_games, lanes=lanes, iterations=sims, seed=7, search_threads=4,
                           max_games=4 * n_games, cross_dedup=cross, blocks_per_tree=bpt, lane_sizes=sizes)
         assert eng.cross_dedup == cross and eng.leaf_dedup
