@@ -41,4 +41,4 @@ def main(fetch_csv, write_csv, out_json, lanes="1", last="0", kernel="k_tower_dy
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:6])
+    main(*sys.argv[1:7])
