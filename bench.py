@@ -336,6 +336,13 @@ def main():
     ap.add_argument("--twin-no-dedup", type=int, default=5, metavar="PLIES",
                     help="after the timed region, turn leaf dedup off and time PLIES more plies of the same games "
                          "(every leaf its own row, as the reference): reported as no_dedup_twin")
+    ap.add_argument("--eval-cache", type=int, default=1, metavar="PLIES",
+                    help="evaluation cache window (include/spmcts.h spmcts_set_eval_cache): a position evaluated in "
+                         "the last PLIES plies takes the cached outputs instead of a network row; 1 (default) = "
+                         "within the ply, so every output a timed ply uses was computed in that ply; 0 = off")
+    ap.add_argument("--twin-no-cache", type=int, default=5, metavar="PLIES",
+                    help="with --eval-cache: after the timed region time PLIES more plies with the cache off "
+                         "(per-step leaf dedup alone): reported as no_cache_twin")
     ap.add_argument("--no-clock", action="store_true",
                     help="do not sample the gfx clock (amdsmi) during the timed region")
     ap.add_argument("--progress", action="store_true",
@@ -398,7 +405,8 @@ def main():
     tdt = {"bf16": torch.bfloat16, "fp16": torch.float16}[args.dtype]
     kw = dict(iterations=args.sims, seed=1234 + rank, device=dev, bucket=args.bucket, opponent=opponent, dtype=tdt,
               evaluate=arena_mode, record=not arena_mode, search_threads=args.search_threads,
-              blocks_per_tree=args.blocks_per_tree, leaf_dedup=False if args.no_leaf_dedup else None)
+              blocks_per_tree=args.blocks_per_tree, leaf_dedup=False if args.no_leaf_dedup else None,
+              eval_cache=0 if (args.no_leaf_dedup or arena_mode or args.search_threads < 2) else args.eval_cache)
     if args.lanes > 1:
         lane_sizes = None
         share = args.lane0_share
@@ -575,6 +583,7 @@ def main():
             "search_threads": args.search_threads,
             "leaf_dedup": bool(getattr(eng, "leaf_dedup", False)),
             "cross_lane_dedup": bool(getattr(eng, "cross_dedup", False)),
+            "eval_cache_plies": int(getattr(eng, "eval_cache", 0)),
         },
         "roofline": {
             "kernel": f"tower::k_tower_dyn (fused ResNet-{4 * args.filter_factor}x{args.blocks} trunk, {args.dtype} MFMA)",
@@ -631,6 +640,7 @@ def main():
             "leaves": leaves,
             "leaf_dedup": bool(getattr(eng, "leaf_dedup", False)),
             "rows_per_leaf": rows / max(1, leaves),
+            "cache_rows": c1["cache_rows"] - c0["cache_rows"],
             "nn_ms": nn_ms,
             "share_of_step": nn_ms / 1e3 / elapsed if elapsed else None,
         },
@@ -668,20 +678,17 @@ def main():
                                      f"games per GPU, policy ResNet-{4 * args.filter_factor}x{args.blocks} (seed 0) vs "
                                      f"opponent (seed 1), evaluate mode (temp/20, noise on), no Move records")
     out["cpu_baseline"] = cpu
-    if args.twin_no_dedup > 0 and getattr(eng, "leaf_dedup", False):
-        # the same arenas, right after the timed region: every leaf gets its own network row
-        for e in getattr(eng, "lanes", [eng]):
-            e.arena.set_leaf_dedup(False)
-            e.leaf_dedup = False
-        eng.leaf_dedup = False
+
+    def twin(plies):
+        """`plies` more plies on the same arenas right after the timed region: (positions/s, ms per ply, rows per leaf)."""
         eng.check()
         t_c0 = eng.counters()
         D.barrier()
         torch.cuda.synchronize()
         t_t0 = time.perf_counter()
-        for _ in range(args.twin_no_dedup):
+        for _ in range(plies):
             one_step()
-        if D.is_distributed() and args.twin_no_dedup % args.exchange_every:
+        if D.is_distributed() and plies % args.exchange_every:
             ex.end_ply(eng.stats_vector, force=True)
         D.barrier()
         torch.cuda.synchronize()
@@ -689,9 +696,27 @@ def main():
         t_c1 = eng.counters()
         eng.check()
         t_moves = int(D.all_reduce_stats([t_c1["moves"] - t_c0["moves"]])[0])
+        return (t_moves / t_el, t_el / plies * 1e3,
+                (t_c1["nn_rows"] - t_c0["nn_rows"]) / max(1, t_c1["nn_leaves"] - t_c0["nn_leaves"]))
+
+    if args.twin_no_cache > 0 and getattr(eng, "eval_cache", 0):
+        for e in getattr(eng, "lanes", [eng]):
+            e.arena.set_eval_cache(0)
+            e.eval_cache = 0
+        v_, ms_, rpl_ = twin(args.twin_no_cache)
+        out["no_cache_twin"] = {
+            "plies": args.twin_no_cache, "value": v_, "ms_per_step": ms_, "rows_per_leaf": rpl_,
+            "note": "the plies right after the timed region, evaluation cache off (spmcts_set_eval_cache 0): leaf "
+                    "dedup within each simulation step only"}
+    if args.twin_no_dedup > 0 and getattr(eng, "leaf_dedup", False):
+        # the same arenas, right after the timed region: every leaf gets its own network row
+        for e in getattr(eng, "lanes", [eng]):
+            e.arena.set_leaf_dedup(False)
+            e.leaf_dedup = False
+        eng.leaf_dedup = False
+        v_, ms_, rpl_ = twin(args.twin_no_dedup)
         out["no_dedup_twin"] = {
-            "plies": args.twin_no_dedup, "value": t_moves / t_el, "ms_per_step": t_el / args.twin_no_dedup * 1e3,
-            "rows_per_leaf": (t_c1["nn_rows"] - t_c0["nn_rows"]) / max(1, t_c1["nn_leaves"] - t_c0["nn_leaves"]),
+            "plies": args.twin_no_dedup, "value": v_, "ms_per_step": ms_, "rows_per_leaf": rpl_,
             "note": "the plies right after the timed region, leaf dedup off (spmcts_set_leaf_dedup): every leaf "
                     "evaluated in its own row, as the reference's InferenceWorker"}
     if args.secondary and not arena_mode:

@@ -118,6 +118,7 @@ typedef struct spmcts_counters {
   int64_t compactions;         /* subtree recyclings (node-store compactions before a search; only
                                   when blocks_per_tree is below the worst case)                 */
   int64_t nn_rows;             /* network rows emitted (= nn_leaves unless leaf dedup is on)  */
+  int64_t cache_rows;          /* leaf rows served from the evaluation cache (spmcts_set_eval_cache) */
 } spmcts_counters;
 
 /* ---- library ------------------------------------------------------------ */
@@ -213,6 +214,20 @@ int spmcts_set_leaf_peer(spmcts_arena *h, spmcts_arena *leader);
  * leader-served step without it fails (-4). */
 int spmcts_peer_push(spmcts_arena *h, float *probs_dev, float *values_dev, const float *leader_probs_dev,
                      const float *leader_values_dev, spmcts_stream stream, spmcts_stream leader_stream);
+/* Evaluation cache (round 6; search_threads > 1 with leaf dedup on, single-network arenas): the network
+ * outputs of the arena's own leaf rows are kept, keyed like leaf dedup ((own, opp) stones from the mover's
+ * view), for `window` generations -- one generation per spmcts_games_begin_ply / spmcts_search_begin, so
+ * window 1 = within the ply (search) that evaluated them.  An owner leaf whose key is cached takes a row
+ * after the network rows (and a follower's leader-served rows) and, at spmcts_expand / spmcts_expand2, the
+ * cached outputs are written into that row of probs / values (k_cache_io), and the rows the network (or the
+ * leader) filled go into the cache.  The reference evaluates every leaf (inference_worker.py:89-119); with
+ * a deterministic, batch-independent evaluator every leaf still receives exactly its own outputs.  After the
+ * network's weights change call spmcts_eval_cache_clear.  window 0 turns it off; capacity_log2 = log2 of the
+ * table's entries (10..28; 0 = twice the rows one window can hold), allocated here (24 + 4 (A + 1) bytes
+ * per entry + 4 per pending slot, outside spmcts_arena_bytes).  (sync) */
+int spmcts_set_eval_cache(spmcts_arena *h, int32_t window, int32_t capacity_log2);
+/* Every cached output leaves the window (host-side generation step; no device work). */
+int spmcts_eval_cache_clear(spmcts_arena *h);
 /* MCTreeSearch._play (mcts.py:272-299) for the active trees + remove_noise:
  * visit-count^(1/temp) distribution, np.random.choice semantics, Move record.
  * Outputs per active tree i: actions_dev[i], states_dev[i][W*H] (int8, tree

@@ -72,6 +72,7 @@ class Counters(ctypes.Structure):
         ("leaked_sims", ctypes.c_int64),
         ("compactions", ctypes.c_int64),
         ("nn_rows", ctypes.c_int64),
+        ("cache_rows", ctypes.c_int64),
     ]
 
     def as_dict(self):
@@ -126,6 +127,8 @@ _SIGS = {
     "spmcts_set_leaf_dedup": [_P, _I32],
     "spmcts_set_leaf_peer": [_P, _P],
     "spmcts_peer_push": [_P, _P, _P, _P, _P, _P, _P],
+    "spmcts_set_eval_cache": [_P, _I32, _I32],
+    "spmcts_eval_cache_clear": [_P],
     "spmcts_leaf_trees": [_P, _P, _P],
     "spmcts_copy_probe": [_P, _P, _U64, _P],
     "spmcts_conv3x3_supported": [_I32, _I32, _I32, _I32],

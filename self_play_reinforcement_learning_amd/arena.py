@@ -226,6 +226,18 @@ class Arena:
         call("spmcts_peer_push", self.h, ptr(probs), ptr(values), ptr(leader_probs), ptr(leader_values), _stream(),
              ctypes.c_void_p(leader_stream.cuda_stream))
 
+    def set_eval_cache(self, window, capacity_log2=0):
+        """Evaluation cache (include/spmcts.h spmcts_set_eval_cache): a leaf whose network input this arena
+        evaluated in the last `window` plies (searches) takes those outputs instead of a row of its own; 0 =
+        off.  Needs leaf dedup; single-network arenas (elsewhere it stays idle).  Same evaluator contract as
+        leaf dedup (pure, batch-independent); call eval_cache_clear() when the weights change."""
+        torch.cuda.current_stream().synchronize()
+        call("spmcts_set_eval_cache", self.h, int(window), int(capacity_log2))
+        self.eval_cache = int(window)
+
+    def eval_cache_clear(self):
+        call("spmcts_eval_cache_clear", self.h)
+
     def set_tapes(self, tapes):
         """Parity mode: one flat float64 stream per tree (list indexed by tree id)."""
         offs = np.zeros(self.n_trees + 1, dtype=np.int64)

@@ -128,6 +128,16 @@ struct View {
   int32_t *xpeer;
   int lead;     // 1: this arena has followers (k_dedup_owner writes okey)
   int peer_on;  // 1 in a follower's simulation-step launches (k_scan_need numbers down-2 slots after its own rows)
+  // evaluation cache (round 6, spmcts_set_eval_cache): network outputs of the arena's own rows kept for `cwin`
+  // generations (one per ply / search), keyed like the dedup table; an owner slot whose key is there takes
+  // the cached outputs (down 3, xc = the entry) in a row after the network rows, filled by k_cache_io.
+  // ctag: (generation << 32 | 1) per entry, 0 = never used; ckey: 2 x u64; cout: A probs + value
+  uint64_t *ctag, *ckey;
+  float *cout;
+  int32_t *xc;
+  int cwin, cmask;  // cwin 0 = off (also in launches where the cache is not live)
+  uint32_t cgen;
+  int served;  // 1: k_scan_need numbers down-2 / down-3 slots after the network rows (peer_on or the cache)
   float *root_prior;
   uint32_t *err;
   // games
@@ -1359,12 +1369,47 @@ __global__ __launch_bounds__(256) void k_dedup_insert(View v) {
 // instead of a dependent dent -> dtab chain per slot in its serial chunk loop); a leader lane also
 // keeps each owner's key for its followers' lookups this step (okey: nothing else writes it until its
 // next step's k_dedup_owner, which runs after every follower's lookup of this step)
+// Evaluation cache (spmcts_set_eval_cache): linear probing over at most CACHE_PROBES entries from the key's
+// hash.  An insert takes the first entry that was never used (tag 0) or whose generation left the window, so
+// every entry before a live key's entry has been in use since that key went in (tags never return to 0):
+// a lookup may stop at the first never-used entry.  Within one arena every lookup (launch_rows) and every
+// insert / fill (k_cache_io, at the expand) is ordered on the arena's stream, and an insert never takes an
+// entry inside the window, so a hit's outputs stay in place until its fill has read them.
+constexpr int CACHE_PROBES = 32;
+
+__device__ __forceinline__ bool cache_live_tag(const View &v, unsigned long long tag) {
+  return tag != 0 && v.cgen - (uint32_t)(tag >> 32) < (uint32_t)v.cwin;
+}
+
+__device__ __forceinline__ int cache_find(const View &v, uint64_t own, uint64_t opp) {
+  uint32_t h = leaf_hash(own, opp) & (uint32_t)v.cmask;
+  for (int p = 0; p < CACHE_PROBES; ++p) {
+    const unsigned long long tag = v.ctag[h];
+    if (tag == 0) return -1;
+    if (cache_live_tag(v, tag) && v.ckey[2 * (size_t)h] == own && v.ckey[2 * (size_t)h + 1] == opp) return (int)h;
+    h = (h + 1) & (uint32_t)v.cmask;
+  }
+  return -1;
+}
+
+// an owner slot's key in the cache: down 3, the entry in xc, its generation renewed (kept while in use)
+template <class G>
+__device__ __forceinline__ bool cache_hit(const View &v, int t) {
+  uint64_t own, opp;
+  leaf_key<G>(v, t, own, opp);
+  const int e = cache_find(v, own, opp);
+  if (e < 0) return false;
+  v.ctag[e] = ((unsigned long long)v.cgen << 32) | 1ull;
+  v.xc[t] = e;
+  return true;
+}
+
 template <class G>
 __global__ __launch_bounds__(256) void k_dedup_owner(View v) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= v.NS) return;
   const bool own = v.need[t] && (int)(uint32_t)v.dtab[v.dent[t]] == t;
-  v.down[t] = own ? 1 : 0;
+  v.down[t] = own ? (v.cwin && cache_hit<G>(v, t) ? 3 : 1) : 0;
   if (own && v.lead) {
     uint64_t a, b;
     leaf_key<G>(v, t, a, b);
@@ -1381,12 +1426,17 @@ __global__ __launch_bounds__(256) void k_dedup_owner(View v) {
 // the outputs its own row would have produced.
 template <class G>
 __global__ __launch_bounds__(256) void k_dedup_owner_peer(View v, const uint64_t *ptab, const uint64_t *pkey,
-                                                          int pmask, uint32_t pgen) {
+                                                          const uint8_t *pdown, int pmask, uint32_t pgen) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= v.NS) return;
   int d = 0, xp = -1;
   if (v.need[t] && (int)(uint32_t)v.dtab[v.dent[t]] == t) {
     d = 1;
+    if (v.cwin && cache_hit<G>(v, t)) {  // the follower's own cache first: no wait on the leader's outputs
+      v.down[t] = 3;
+      v.xpeer[t] = -1;
+      return;
+    }
     uint64_t own, opp;
     leaf_key<G>(v, t, own, opp);
     uint32_t h = leaf_hash(own, opp) & (uint32_t)pmask;
@@ -1395,8 +1445,10 @@ __global__ __launch_bounds__(256) void k_dedup_owner_peer(View v, const uint64_t
       if ((uint32_t)(w >> 32) != pgen) break;  // not in the leader's batch
       const int s = (int)(uint32_t)w;
       if (pkey[2 * (size_t)s] == own && pkey[2 * (size_t)s + 1] == opp) {
-        d = 2;
-        xp = s;
+        if (pdown[s] == 1) {  // a row the leader's network evaluates (not one its cache fills at its expand)
+          d = 2;
+          xp = s;
+        }
         break;
       }
       h = (h + 1) & (uint32_t)pmask;
@@ -1415,6 +1467,48 @@ __global__ __launch_bounds__(256) void k_peer_push(View v, const int32_t *psrow,
   const int r1 = v.srow[t], r0 = psrow[v.xpeer[t]];
   for (int a = 0; a < v.A; ++a) probs[(size_t)r1 * v.A + a] = pprobs[(size_t)r0 * v.A + a];
   values[r1] = pvalues[r0];
+}
+
+// Evaluation cache at the expand of a step whose rows consulted it (single-network arenas): a cache-served
+// owner slot (down 3) gets its entry's outputs in its row; a slot whose row holds network outputs (down 1:
+// its own network's, down 2: the leader's, pushed before this) puts them in the cache under the current
+// generation (nothing is cached when no entry within CACHE_PROBES is free).  Duplicates (down 0) read their
+// owner's row.
+template <class G>
+__global__ __launch_bounds__(256) void k_cache_io(View v, float *probs, float *values) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= v.NS || !v.need[t]) return;
+  const int d = v.down[t];
+  if (d == 0) return;
+  const int r = v.srow[t], A = v.A;
+  float *pr = probs + (size_t)r * A;
+  if (d == 3) {
+    const float *c = v.cout + (size_t)v.xc[t] * (A + 1);
+    for (int a = 0; a < A; ++a) pr[a] = c[a];
+    values[r] = c[A];
+    return;
+  }
+  uint64_t own, opp;
+  leaf_key<G>(v, t, own, opp);
+  uint32_t h = leaf_hash(own, opp) & (uint32_t)v.cmask;
+  const unsigned long long mine = ((unsigned long long)v.cgen << 32) | 1ull;
+  unsigned long long *tag = (unsigned long long *)v.ctag;
+  for (int p = 0; p < CACHE_PROBES; ++p) {
+    unsigned long long w = tag[h];
+    while (!cache_live_tag(v, w)) {  // never used, or outside the window: free to take
+      const unsigned long long old = atomicCAS(tag + h, w, mine);
+      if (old == w) {
+        v.ckey[2 * (size_t)h] = own;
+        v.ckey[2 * (size_t)h + 1] = opp;
+        float *c = v.cout + (size_t)h * (A + 1);
+        for (int a = 0; a < A; ++a) c[a] = pr[a];
+        c[A] = values[r];
+        return;
+      }
+      w = old;  // another slot of this launch took it (now live): probe on
+    }
+    h = (h + 1) & (uint32_t)v.cmask;
+  }
 }
 
 __device__ __forceinline__ bool row_owner(const View &v, int t) { return v.dedup ? v.down[t] == 1 : v.need[t] != 0; }
@@ -1443,14 +1537,15 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_need(View v, int32_t *cou
   const int T = v.NS;  // pending slots (tree * K + j), tree order then in-flight order
   const int chunk = (T + SCAN_THREADS - 1) / SCAN_THREADS;
   const int lo = min(T, tid * chunk), hi = min(T, lo + chunk);
-  int c0 = 0, c1 = 0, c2 = 0;
+  int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
   // unrolled so each thread's chunk of flags is fetched in one round of independent loads
-  if (v.peer_on) {  // a follower's simulation step (single network): own rows, then the leader-served rows
+  if (v.served) {  // single network: own rows, then the leader-served and cache-served rows
 #pragma unroll 16
     for (int t = lo; t < hi; ++t) {
       const int d = v.down[t];
       c0 += d == 1;
-      c2 += d == 2;
+      c2 += d >= 2;
+      c3 += d == 3;
     }
   } else {
 #pragma unroll 16
@@ -1499,17 +1594,22 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_need(View v, int32_t *cou
   i1 += wave ? s_w1[wave - 1] : 0;
   i2 += wave ? s_w2[wave - 1] : 0;
   int r0 = i0 - c0, r1 = v.seg1 + i1 - c1;
-  if (v.peer_on) {
-    int r2 = s_w0[SCAN_WAVES - 1] + i2 - c2;  // the leader-served rows follow all own rows
+  if (v.served) {
+    int r2 = s_w0[SCAN_WAVES - 1] + i2 - c2;  // the leader- and cache-served rows follow all own rows
 #pragma unroll 16
     for (int t = lo; t < hi; ++t) {
       const int d = v.down[t];
       if (d == 1) {
         v.row_tree[r0] = t;
         v.srow[t] = r0++;
-      } else if (d == 2) {
+      } else if (d >= 2) {
         v.srow[t] = r2++;
       }
+    }
+    if (v.cwin) {  // cache-served rows (counters.cache_rows)
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) c3 += __shfl_xor(c3, off, 64);
+      if (lane == 0 && c3) atomicAdd((unsigned long long *)&v.gcnt[11], (unsigned long long)c3);
     }
   } else {
 #pragma unroll 16
@@ -2426,6 +2526,10 @@ struct spmcts_arena {
   hipStream_t push_stream = nullptr;  // a follower's stream for k_peer_push (spmcts_peer_push)
   bool peer_step = false;  // the last launch_rows of this follower used the leader's table
   bool push_pending = false;  // the leader's stream has not yet waited for this follower's last push
+  // evaluation cache (spmcts_set_eval_cache): its allocations, and whether the last launch_rows consulted it
+  // (the next expand then runs k_cache_io)
+  std::vector<void *> cache_allocs;
+  bool cache_step = false;
 };
 
 static int geometry(const spmcts_config *c, int *A, int *P, int *cells, int *maxd, int *maxm) {
@@ -2749,6 +2853,7 @@ int spmcts_arena_destroy(spmcts_arena *h) {
     if (e) (void)hipEventDestroy(e);
   if (h->push_stream) (void)hipStreamDestroy(h->push_stream);
   for (void *p : h->allocs) (void)hipFree(p);
+  for (void *p : h->cache_allocs) (void)hipFree(p);
   delete h;
   return 0;
 }
@@ -2862,6 +2967,7 @@ int spmcts_search_begin(spmcts_arena *h, const int32_t *trees_dev, int32_t n, sp
   if (n > std::max(h->v.T, h->v.G)) return fail(-3, "too many active trees");
   h->n_active = n;
   h->v.sim = 0;
+  if (h->v.cwin) ++h->v.cgen;  // a new evaluation-cache generation per search
   if (n <= 0) return 0;
   DISPATCH(h, hipLaunchKernelGGL(k_search_begin<GG>, dim3(nblk(n, 128)), dim3(128), 0, (hipStream_t)stream, h->v,
                                  trees_dev, n));
@@ -2885,6 +2991,10 @@ static int launch_rows(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_de
     }
   View v = h->v;
   v.peer_on = 0;
+  // the evaluation cache is live in leaf-dedup launches of single-network arenas (spmcts_set_eval_cache)
+  h->cache_step = v.cwin > 0 && v.dedup && v.seg1 >= v.NS;
+  if (!h->cache_step) v.cwin = 0;
+  v.served = h->cache_step ? 1 : 0;
   if (v.dedup) {
     if (++h->v.dgen == 0) ++h->v.dgen;  // generation 0 = the zeroed table
     v.dgen = h->v.dgen;
@@ -2896,8 +3006,9 @@ static int launch_rows(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_de
       const spmcts_arena *p = h->peer;
       HIP_TRY(hipStreamWaitEvent(s, p->ev_ins, 0));
       v.peer_on = 1;
+      v.served = 1;
       DISPATCH(h, hipLaunchKernelGGL(k_dedup_owner_peer<GG>, dim3(nblk(v.NS, 256)), dim3(256), 0, s, v,
-                                     p->v.dtab, p->v.okey, p->v.dmask, p->v.dgen));
+                                     p->v.dtab, p->v.okey, p->v.down, p->v.dmask, p->v.dgen));
     } else {
       DISPATCH(h, hipLaunchKernelGGL(k_dedup_owner<GG>, dim3(nblk(v.NS, 256)), dim3(256), 0, s, v));
     }
@@ -2979,6 +3090,11 @@ int spmcts_expand2(spmcts_arena *h, const float *probs0_dev, const float *values
   if (h->peer_step) return fail(-4, "a follower lane's simulation step needs spmcts_peer_push before its expand");
   if (h->v.seg1 < h->v.NS && (!probs1_dev || !values1_dev))
     return fail(-1, "two-network arena needs network-1 outputs");
+  if (h->cache_step) {  // the rows of this step consulted the evaluation cache: fills and inserts first
+    DISPATCH(h, hipLaunchKernelGGL(k_cache_io<GG>, dim3(nblk(h->v.NS, 256)), dim3(256), 0, (hipStream_t)stream, h->v,
+                                   (float *)probs0_dev, (float *)values0_dev));
+    h->cache_step = false;
+  }
   const int gpb = 64 / h->P;
   if (h->v.K > 1) {
     const int tb = h->tree_block, tpb = tb / h->P;
@@ -3085,6 +3201,61 @@ int spmcts_set_leaf_dedup(spmcts_arena *h, int32_t on) {
   return 0;
 }
 
+int spmcts_set_eval_cache(spmcts_arena *h, int32_t window, int32_t capacity_log2) {
+  if (!h) return fail(-1, "null arena");
+  if (window < 0 || window > (1 << 20)) return fail(-3, "eval cache window out of range");
+  if (capacity_log2 != 0 && (capacity_log2 < 10 || capacity_log2 > 28)) return fail(-3, "eval cache capacity_log2: 10..28 (0 = sized from the arena)");
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipDeviceSynchronize());  // no launch of this arena reads the old table any more
+  for (void *p : h->cache_allocs) (void)hipFree(p);
+  h->cache_allocs.clear();
+  View &v = h->v;
+  v.ctag = v.ckey = nullptr;
+  v.cout = nullptr;
+  v.xc = nullptr;
+  v.cwin = 0;
+  v.cmask = 0;
+  h->cache_step = false;
+  if (window == 0) return 0;
+  if (v.K < 2) return fail(-3, "the evaluation cache needs search_threads > 1 (it extends leaf dedup)");
+  int L = capacity_log2;
+  if (L == 0) {
+    // entries live in one window: at most one row per searching tree per sim, plus the end-of-ply rows;
+    // twice that, so probe chains stay short
+    const long long searching = std::max<long long>(v.G > 0 ? v.G : v.T, 1);
+    const long long live = (long long)window * searching * ((long long)v.iters + 2);
+    L = 10;
+    while (L < 26 && (1ll << L) < 2 * live) ++L;
+  }
+  const size_t E = (size_t)1 << L;
+  void *p[4] = {};
+  const size_t bytes[4] = {E * 8, E * 16, E * sizeof(float) * (h->A + 1), (size_t)v.NS * 4};
+  for (int i = 0; i < 4; ++i) {
+    const hipError_t e = hipMalloc(&p[i], bytes[i]);
+    if (e != hipSuccess) {
+      for (int j = 0; j < i; ++j) (void)hipFree(p[j]);
+      return fail(-1000 - (int)e, std::string("eval cache hipMalloc: ") + hipGetErrorString(e));
+    }
+    h->cache_allocs.push_back(p[i]);
+  }
+  HIP_TRY(hipMemset(p[0], 0, bytes[0]));  // every entry never used
+  v.ctag = (uint64_t *)p[0];
+  v.ckey = (uint64_t *)p[1];
+  v.cout = (float *)p[2];
+  v.xc = (int32_t *)p[3];
+  v.cmask = (int)(E - 1);
+  v.cwin = window;
+  v.cgen = (uint32_t)window + 1;  // generation 0 never read as live
+  HIP_TRY(hipDeviceSynchronize());
+  return 0;
+}
+
+int spmcts_eval_cache_clear(spmcts_arena *h) {
+  if (!h) return fail(-1, "null arena");
+  if (h->v.cwin) h->v.cgen += (uint32_t)h->v.cwin + 1;  // every entry leaves the window
+  return 0;
+}
+
 int spmcts_games_set_record(spmcts_arena *h, int32_t record) {
   if (!h) return fail(-1, "null arena");
   h->v.record = record ? 1 : 0;
@@ -3182,6 +3353,7 @@ int spmcts_games_begin_ply(spmcts_arena *h, spmcts_stream stream) {
   if (h->v.G <= 0) return fail(-4, "arena has no game slots");
   h->n_active = h->v.G;
   h->v.sim = 0;
+  if (h->v.cwin) ++h->v.cgen;  // a new evaluation-cache generation per ply
   DISPATCH(h, hipLaunchKernelGGL(k_games_begin_ply<GG>, dim3(nblk(h->v.G, 128)), dim3(128), 0, (hipStream_t)stream,
                                  h->v));
   if (h->v.gc)
@@ -3257,6 +3429,7 @@ int spmcts_get_counters(spmcts_arena *h, spmcts_counters *out) {
   for (int k = 0; k < 6; ++k) out->results[k / 3][k % 3] = g[1 + k];
   out->positions_exported = g[9];
   out->nn_rows = g[10];
+  out->cache_rows = g[11];
   HIP_TRY(hipMemcpy(&out->error_flags, h->v.err, 4, hipMemcpyDeviceToHost));
   return 0;
 }

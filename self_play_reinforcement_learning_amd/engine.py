@@ -89,11 +89,14 @@ class SelfPlayEngine:
                  seed=0, subsequence0=None, rng="philox", max_games=None, device=None, dtype=torch.float16,
                  leaf_layout="nhwc", cpuct=4.0, x_noise=0.25, blocks_per_tree=0, bucket=256, opponent=None,
                  opponent_iterations=None, record=True, search_threads=1, leaf_dedup=None, opponent_alpha=None,
-                 opponent_strong_play=None, opponent_search_threads=None):
+                 opponent_strong_play=None, opponent_search_threads=None, eval_cache=None):
         """opponent_alpha / opponent_strong_play / opponent_search_threads: the opposing MCTS side's own
         search settings (evaluation games: each side is built from its own container's kwargs,
         selfplayworker.py:71-81); None = the policy's.  dtype: the fused trunk's element type, fp16 by
-        default (the reference's inference autocast, inference_worker.py:114-119) or bf16."""
+        default (the reference's inference autocast, inference_worker.py:114-119) or bf16.  eval_cache: plies
+        a position's network outputs stay cached (include/spmcts.h spmcts_set_eval_cache; 0 = off, 1 = within
+        the ply that evaluated them); needs leaf dedup (a pure evaluator, search_threads > 1) and one network;
+        None = 1 where those hold, else 0."""
         self.game = game
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.evaluator = make_evaluator(network, game, device=self.device, dtype=dtype, leaf_layout=leaf_layout)
@@ -155,6 +158,13 @@ class SelfPlayEngine:
         self.leaf_dedup = bool(pure if leaf_dedup is None else leaf_dedup) and self.search_threads > 1
         if self.leaf_dedup:
             self.arena.set_leaf_dedup(True)
+        # evaluation cache (include/spmcts.h spmcts_set_eval_cache): the dedup key extended over plies
+        cache_ok = self.leaf_dedup and self.evaluator1 is None
+        self.eval_cache = (1 if cache_ok else 0) if eval_cache is None else int(eval_cache)
+        if self.eval_cache and not cache_ok:
+            raise ValueError("eval_cache needs leaf dedup (a pure evaluator, search_threads > 1) and a single network")
+        if self.eval_cache:
+            self.arena.set_eval_cache(self.eval_cache)
         self.n_games = n_games
         self.max_games = max_games
         # torch convolutions want few distinct shapes; the fused HIP tower takes any batch
@@ -189,6 +199,8 @@ class SelfPlayEngine:
         for ev in (self.evaluator, self.evaluator1):
             if ev is not None and hasattr(ev, "refresh"):
                 ev.refresh()
+        if self.eval_cache:
+            self.arena.eval_cache_clear()  # outputs of the old weights leave the cache
         self.refresh_root_prior()
 
     def enable_timers(self, on=True):
@@ -545,6 +557,7 @@ class LanedEngine:
         self.select_steps = self.lanes[0].select_steps
         self.search_threads = self.lanes[0].search_threads
         self.leaf_dedup = self.lanes[0].leaf_dedup
+        self.eval_cache = self.lanes[0].eval_cache
         self.evaluator = self.lanes[0].evaluator
         self.select_timer = self.expand_timer = self.nn_timer = self.tower_timer = None
 

@@ -689,7 +689,7 @@ def test_leaf_dedup_is_exact(game, n_games, sims, bpt):
     out = []
     for dedup in (False, True):
         eng = SelfPlayEngine(game, net, n_games=n_games, iterations=sims, seed=3, max_games=2 * n_games,
-                             search_threads=4, leaf_dedup=dedup, blocks_per_tree=bpt)
+                             search_threads=4, leaf_dedup=dedup, blocks_per_tree=bpt, eval_cache=0)
         assert eng.leaf_dedup == dedup and eng.evaluator.pure_planes
         out.append(_run_moves(eng, 2 * n_games))
     (m0, c0), (m1, c1) = out
@@ -724,7 +724,8 @@ def test_cross_lane_dedup_is_exact(lanes, n_games, sims, game, bpt, sizes):
         # (TicTacToe; a recycled node store beside the pairing -- 96 blocks per tree: compacted within the 12
         # plies --; unequal lanes, as bench.py's 0.48 split)
         eng = LanedEngine(game, net, n_games=n_games, lanes=lanes, iterations=sims, seed=7, search_threads=4,
-                          max_games=4 * n_games, cross_dedup=cross, blocks_per_tree=bpt, lane_sizes=sizes)
+                          max_games=4 * n_games, cross_dedup=cross, blocks_per_tree=bpt, lane_sizes=sizes,
+                          eval_cache=0)
         assert eng.cross_dedup == cross and eng.leaf_dedup
         got = []
         eng.run(plies=12, on_moves=lambda m: got.append({k: v.cpu().numpy() for k, v in m.items()}))
@@ -804,6 +805,136 @@ def test_leaf_dedup_two_networks_exact():
     assert c1["nn_rows"] < c1["nn_leaves"]
 
 
+_SAME = ("sims", "leaked_sims", "moves", "nn_leaves", "terminal_leaves", "depth_sum", "games_finished",
+         "positions_exported", "results")
+
+
+@pytest.mark.parametrize("game,n_games,sims,bpt,window,cap", [("connect4", 512, 16, 0, 1, 0), ("connect4", 512, 16, 0, 3, 0),
+                                                              ("tictactoe", 256, 24, 0, 2, 0),
+                                                              ("connect4", 256, 16, 6 * 16 + 64, 2, 0),
+                                                              ("connect4", 512, 16, 0, 4, 10)])
+def test_eval_cache_is_exact(game, n_games, sims, bpt, window, cap):
+    """Evaluation cache (include/spmcts.h spmcts_set_eval_cache): a leaf whose network input the arena evaluated
+    in the last `window` plies takes those outputs instead of a row.  Nothing a search sees changes: the same
+    Move records bit for bit and the same counters as per-step dedup alone, and every owner row of a step is
+    either evaluated or cache-served (nn_rows + cache_rows = the dedup run's nn_rows); also beside subtree
+    recycling, and with a 1,024-entry table (cap 10) whose inserts collide and run out of free entries."""
+    from self_play_reinforcement_learning_amd.engine import SelfPlayEngine
+    from self_play_reinforcement_learning_amd.modules import ResidualTower
+
+    torch.manual_seed(0)
+    W, H, A = (7, 6, 7) if game == "connect4" else (3, 3, 9)
+    net = ResidualTower(W, H, A, num_blocks=2, filter_factor=32)
+    out = []
+    for w in (0, window):
+        eng = SelfPlayEngine(game, net, n_games=n_games, iterations=sims, seed=3, max_games=2 * n_games,
+                             search_threads=4, blocks_per_tree=bpt, eval_cache=w)
+        assert eng.leaf_dedup and eng.eval_cache == w
+        if w and cap:
+            eng.arena.set_eval_cache(w, cap)
+        out.append(_run_moves(eng, 2 * n_games))
+    (m0, c0), (m1, c1) = out
+    for k in m0:
+        np.testing.assert_array_equal(m0[k], m1[k], err_msg=k)
+    for k in _SAME:
+        assert c0[k] == c1[k], k
+    assert c0["cache_rows"] == 0 and c1["cache_rows"] > 0
+    assert c1["nn_rows"] + c1["cache_rows"] == c0["nn_rows"]
+    assert (c1["compactions"] > 0) == (bpt > 0)
+    print(f"eval cache, {game} window {window} cap {cap}: rows/leaf {c0['nn_rows'] / c0['nn_leaves']:.4f} -> "
+          f"{c1['nn_rows'] / c1['nn_leaves']:.4f}")
+
+
+@pytest.mark.parametrize("lanes,sizes", [(2, None), (3, None), (2, [118, 138])])
+def test_eval_cache_with_cross_lane_dedup_is_exact(lanes, sizes):
+    """The evaluation cache beside cross-lane dedup: a follower looks in its own cache first, then in the leader's
+    batch (only rows the leader's network evaluates serve it).  Every lane's Move records and the counters equal
+    those of per-step dedup alone; fewer network rows than cross-lane dedup alone."""
+    from self_play_reinforcement_learning_amd.engine import LanedEngine
+    from self_play_reinforcement_learning_amd.modules import ResidualTower
+
+    torch.manual_seed(0)
+    net = ResidualTower(7, 6, 7, num_blocks=2, filter_factor=32).cuda().eval()
+    n_games = 256 if sizes else 128 * lanes
+    out = []
+    for cross, w in ((False, 0), (True, 0), (True, 2)):
+        eng = LanedEngine("connect4", net, n_games=n_games, lanes=lanes, iterations=16, seed=7, search_threads=4,
+                          max_games=4 * n_games, cross_dedup=cross, lane_sizes=sizes, eval_cache=w)
+        assert eng.cross_dedup == cross and eng.eval_cache == w
+        got = []
+        eng.run(plies=12, on_moves=lambda m: got.append({k: v.cpu().numpy() for k, v in m.items()}))
+        eng.check()
+        out.append(({k: np.concatenate([g[k] for g in got]) for k in got[0]}, eng.counters()))
+    (m0, c0), (m1, c1), (m2, c2) = out
+    for k in m0:
+        np.testing.assert_array_equal(m0[k], m2[k], err_msg=k)
+        np.testing.assert_array_equal(m1[k], m2[k], err_msg=k)
+    for k in _SAME:
+        assert c0[k] == c2[k] and c1[k] == c2[k], k
+    assert c2["cache_rows"] > 0 and c2["nn_rows"] < c1["nn_rows"] < c0["nn_rows"]
+    print(f"eval cache + cross-lane dedup, {lanes} lanes: rows/leaf {c1['nn_rows'] / c1['nn_leaves']:.4f} -> "
+          f"{c2['nn_rows'] / c2['nn_leaves']:.4f}")
+
+
+def test_eval_cache_cleared_on_new_weights():
+    """refresh_network after the weights change clears the cache (spmcts_eval_cache_clear): the plies after the
+    change see the new network's outputs only, exactly as the run without a cache does."""
+    from self_play_reinforcement_learning_amd.engine import SelfPlayEngine
+    from self_play_reinforcement_learning_amd.modules import ResidualTower
+
+    out = []
+    for w in (0, 8):
+        torch.manual_seed(0)
+        net = ResidualTower(7, 6, 7, num_blocks=2, filter_factor=32).cuda().eval()
+        torch.manual_seed(1)
+        new = ResidualTower(7, 6, 7, num_blocks=2, filter_factor=32).cuda().eval()
+        eng = SelfPlayEngine("connect4", net, n_games=256, iterations=16, seed=11, search_threads=4, eval_cache=w)
+        got = []
+        sink = lambda m: got.append({k: v.cpu().numpy() for k, v in m.items()})  # noqa: E731
+        eng.run(plies=10, on_moves=sink)
+        net.load_state_dict(new.state_dict())
+        eng.refresh_network()
+        eng.run(plies=10, on_moves=sink)
+        eng.check()
+        out.append(({k: np.concatenate([g[k] for g in got]) for k in got[0]}, eng.counters()))
+    (m0, c0), (m1, c1) = out
+    for k in m0:
+        np.testing.assert_array_equal(m0[k], m1[k], err_msg=k)
+    for k in _SAME:
+        assert c0[k] == c1[k], k
+    assert c1["cache_rows"] > 0
+
+
+def test_eval_cache_rules():
+    """spmcts_set_eval_cache refuses what it cannot serve exactly: search_threads 1 (no dedup rows) and a bad
+    capacity; SelfPlayEngine refuses it without leaf dedup or with two networks."""
+    from self_play_reinforcement_learning_amd import _lib
+    from self_play_reinforcement_learning_amd.arena import Arena
+    from self_play_reinforcement_learning_amd.engine import SelfPlayEngine
+    from self_play_reinforcement_learning_amd.modules import ResidualTower
+
+    a = Arena("connect4", n_trees=64, iterations=8, search_threads=1, leaf_format="f32")
+    with pytest.raises(_lib.SpmctsError, match="search_threads"):
+        a.set_eval_cache(1)
+    a.set_eval_cache(0)
+    a.close()
+    b = Arena("connect4", n_trees=64, iterations=8, search_threads=4, leaf_format="f32")
+    with pytest.raises(_lib.SpmctsError, match="capacity"):
+        b.set_eval_cache(1, 40)
+    b.set_eval_cache(2, 12)
+    b.eval_cache_clear()
+    b.close()
+    torch.manual_seed(0)
+    net = ResidualTower(7, 6, 7, num_blocks=2, filter_factor=32)
+    with pytest.raises(ValueError, match="eval_cache"):
+        SelfPlayEngine("connect4", net, n_games=64, iterations=8, search_threads=4, leaf_dedup=False, eval_cache=1)
+    torch.manual_seed(1)
+    opp = ResidualTower(7, 6, 7, num_blocks=2, filter_factor=32)
+    with pytest.raises(ValueError, match="eval_cache"):
+        SelfPlayEngine("connect4", net, n_games=64, iterations=8, search_threads=4, opponent=opp, evaluate=True,
+                       eval_cache=1)
+
+
 def test_bench_line_small_with_no_dedup_twin():
     """bench.py end to end on a small workload (subprocess, as the driver runs it): one JSON line with
     the contract keys, roofline and tree roofline, and the --twin-no-dedup plies (leaf dedup off on
@@ -833,3 +964,23 @@ def test_bench_line_small_with_no_dedup_twin():
     r = d["ranks"]
     assert r["world_size"] == 1 and len(r["per_rank"]) == 1
     assert r["positions_per_s_min"] == r["positions_per_s_max"] == r["per_rank"][0]["positions_per_s"]
+
+
+def test_bench_line_small_with_eval_cache():
+    """bench.py --eval-cache: the line names the window, counts the cache-served rows, and carries the
+    no_cache_twin (the plies after the timed region with the cache off: per-step dedup alone, more rows)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--games", "512", "--sims", "16", "--blocks", "2",
+           "--steps", "3", "--warmup", "2", "--no-cpu-baseline", "--eval-cache", "2", "--twin-no-cache", "2",
+           "--twin-no-dedup", "2"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=root, check=True).stdout
+    d = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
+    assert d["config"]["eval_cache_plies"] == 2 and d["nn"]["cache_rows"] > 0
+    tw, td = d["no_cache_twin"], d["no_dedup_twin"]
+    assert tw["plies"] == 2 and tw["value"] > 0 and d["nn"]["rows_per_leaf"] < tw["rows_per_leaf"] < 1.0
+    assert td["rows_per_leaf"] == 1.0

@@ -31,7 +31,8 @@ def test_library_exports_every_header_symbol():
 def test_config_struct_layout():
     # 14 x int32 + 3 x double + 2 x uint64 = 56 + 24 + 16
     assert ctypes.sizeof(_lib.Config) == 96
-    assert ctypes.sizeof(_lib.Counters) == 8 * 8 + 6 * 8 + 8 + 8 + 8 + 8 + 8  # ..., error_flags, reserved, leaked_sims, compactions, nn_rows
+    # ..., error_flags, reserved, leaked_sims, compactions, nn_rows, cache_rows
+    assert ctypes.sizeof(_lib.Counters) == 8 * 8 + 6 * 8 + 8 + 8 + 8 + 8 + 8 + 8
 
 
 @pytest.mark.parametrize("name,game,W,H", [("c4", 0, 7, 6), ("ttt", 1, 3, 3)])
