@@ -186,7 +186,7 @@ def lib():
 # SPMCTS_ERR_AB_SWITCH (-5, include/spmcts.h) rather than silently ignoring them
 AB_SWITCHES = ("SPMCTS_TOWER_CG", "SPMCTS_TOWER_RING", "SPMCTS_TOWER_C256", "SPMCTS_WIDE_TAILS", "SPMCTS_HEADS",
                "SPMCTS_HEADS_C256", "SPMCTS_TREE_BLOCK", "SPMCTS_EXPAND_CO", "SPMCTS_TOWER_M16",
-               "SPMCTS_TREE_COPIES", "SPMCTS_PEER_PUSH")
+               "SPMCTS_TREE_COPIES", "SPMCTS_PEER_PUSH", "SPMCTS_CACHE_SHARE")
 ERR_AB_SWITCH = -5
 
 

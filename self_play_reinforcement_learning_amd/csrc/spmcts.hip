@@ -137,6 +137,7 @@ struct View {
   int32_t *xc;
   int cwin, cmask;  // cwin 0 = off (also in launches where the cache is not live)
   uint32_t cgen;
+  int cshared;  // 1: a follower lane using its leader's table (the leader inserts the rows it serves)
   int served;  // 1: k_scan_need numbers down-2 / down-3 slots after the network rows (peer_on or the cache)
   float *root_prior;
   uint32_t *err;
@@ -1370,21 +1371,36 @@ __global__ __launch_bounds__(256) void k_dedup_insert(View v) {
 // keeps each owner's key for its followers' lookups this step (okey: nothing else writes it until its
 // next step's k_dedup_owner, which runs after every follower's lookup of this step)
 // Evaluation cache (spmcts_set_eval_cache): linear probing over at most CACHE_PROBES entries from the key's
-// hash.  An insert takes the first entry that was never used (tag 0) or whose generation left the window, so
-// every entry before a live key's entry has been in use since that key went in (tags never return to 0):
-// a lookup may stop at the first never-used entry.  Within one arena every lookup (launch_rows) and every
-// insert / fill (k_cache_io, at the expand) is ordered on the arena's stream, and an insert never takes an
-// entry inside the window, so a hit's outputs stay in place until its fill has read them.
+// hash.  An entry's tag is (generation << 32 | state): 0 = never used, CACHE_READY = key and outputs published,
+// CACHE_BUSY = being written.  A lookup sees READY entries whose generation is within the window of its own
+// (0 <= cgen - gen < cwin); an insert may take an entry that was never used or whose READY generation is more
+// than cwin behind its own (one generation of slack: the two lanes of a shared table are at most one ply apart,
+// so no entry a lane can still see, or renew, is taken by the other).  Tags never return to 0, so every entry
+// before a live key's entry in its probe chain has been in use since the key went in, and a lookup may stop at
+// the first never-used entry.  Publication: CAS to BUSY, key and outputs stored, then the READY tag stored with
+// release semantics (agent scope); lookups load tags with acquire semantics, so a READY key is never read torn
+// (a lane sharing its leader's table reads it while the leader's expand inserts on another stream).
 constexpr int CACHE_PROBES = 32;
+constexpr unsigned long long CACHE_READY = 1ull, CACHE_BUSY = 2ull;
+
+__device__ __forceinline__ unsigned long long cache_tag_load(const View &v, uint32_t h) {
+  return __hip_atomic_load((unsigned long long *)v.ctag + h, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 __device__ __forceinline__ bool cache_live_tag(const View &v, unsigned long long tag) {
-  return tag != 0 && v.cgen - (uint32_t)(tag >> 32) < (uint32_t)v.cwin;
+  const int d = (int)(v.cgen - (uint32_t)(tag >> 32));
+  return (tag & 0xffffffffull) == CACHE_READY && d >= 0 && d < v.cwin;
+}
+
+__device__ __forceinline__ bool cache_free_tag(const View &v, unsigned long long tag) {
+  const int d = (int)(v.cgen - (uint32_t)(tag >> 32));
+  return tag == 0 || ((tag & 0xffffffffull) == CACHE_READY && d > v.cwin);
 }
 
 __device__ __forceinline__ int cache_find(const View &v, uint64_t own, uint64_t opp) {
   uint32_t h = leaf_hash(own, opp) & (uint32_t)v.cmask;
   for (int p = 0; p < CACHE_PROBES; ++p) {
-    const unsigned long long tag = v.ctag[h];
+    const unsigned long long tag = cache_tag_load(v, h);
     if (tag == 0) return -1;
     if (cache_live_tag(v, tag) && v.ckey[2 * (size_t)h] == own && v.ckey[2 * (size_t)h + 1] == opp) return (int)h;
     h = (h + 1) & (uint32_t)v.cmask;
@@ -1399,7 +1415,8 @@ __device__ __forceinline__ bool cache_hit(const View &v, int t) {
   leaf_key<G>(v, t, own, opp);
   const int e = cache_find(v, own, opp);
   if (e < 0) return false;
-  v.ctag[e] = ((unsigned long long)v.cgen << 32) | 1ull;
+  __hip_atomic_store((unsigned long long *)v.ctag + e, ((unsigned long long)v.cgen << 32) | CACHE_READY,
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   v.xc[t] = e;
   return true;
 }
@@ -1471,9 +1488,9 @@ __global__ __launch_bounds__(256) void k_peer_push(View v, const int32_t *psrow,
 
 // Evaluation cache at the expand of a step whose rows consulted it (single-network arenas): a cache-served
 // owner slot (down 3) gets its entry's outputs in its row; a slot whose row holds network outputs (down 1:
-// its own network's, down 2: the leader's, pushed before this) puts them in the cache under the current
-// generation (nothing is cached when no entry within CACHE_PROBES is free).  Duplicates (down 0) read their
-// owner's row.
+// its own network's, down 2: the leader's, pushed before this -- unless the table is the leader's own, which
+// the leader fills) puts them in the cache under the current generation (nothing is cached when no entry
+// within CACHE_PROBES is free).  Duplicates (down 0) read their owner's row.
 template <class G>
 __global__ __launch_bounds__(256) void k_cache_io(View v, float *probs, float *values) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1488,24 +1505,26 @@ __global__ __launch_bounds__(256) void k_cache_io(View v, float *probs, float *v
     values[r] = c[A];
     return;
   }
+  if (d == 2 && v.cshared) return;
   uint64_t own, opp;
   leaf_key<G>(v, t, own, opp);
   uint32_t h = leaf_hash(own, opp) & (uint32_t)v.cmask;
-  const unsigned long long mine = ((unsigned long long)v.cgen << 32) | 1ull;
+  const unsigned long long gen = (unsigned long long)v.cgen << 32;
   unsigned long long *tag = (unsigned long long *)v.ctag;
   for (int p = 0; p < CACHE_PROBES; ++p) {
-    unsigned long long w = tag[h];
-    while (!cache_live_tag(v, w)) {  // never used, or outside the window: free to take
-      const unsigned long long old = atomicCAS(tag + h, w, mine);
+    unsigned long long w = cache_tag_load(v, h);
+    while (cache_free_tag(v, w)) {  // never used, or behind the window (+1): free to take
+      const unsigned long long old = atomicCAS(tag + h, w, gen | CACHE_BUSY);
       if (old == w) {
         v.ckey[2 * (size_t)h] = own;
         v.ckey[2 * (size_t)h + 1] = opp;
         float *c = v.cout + (size_t)h * (A + 1);
         for (int a = 0; a < A; ++a) c[a] = pr[a];
         c[A] = values[r];
+        __hip_atomic_store(tag + h, gen | CACHE_READY, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }
-      w = old;  // another slot of this launch took it (now live): probe on
+      w = old;  // another insert took it first: probe on
     }
     h = (h + 1) & (uint32_t)v.cmask;
   }
@@ -2530,7 +2549,38 @@ struct spmcts_arena {
   // (the next expand then runs k_cache_io)
   std::vector<void *> cache_allocs;
   bool cache_step = false;
+  bool cache_shared_step = false;  // that launch used the leader's table (cache_view)
+  const uint64_t *cache_tab = nullptr;  // the table that launch looked its keys up in
 };
+
+// The evaluation-cache table of a launch: a follower lane (spmcts_set_leaf_peer) whose leader runs a cache of
+// the same window, one generation apart at most, uses the leader's table -- one table for the GPU's lanes, so a
+// position either lane evaluated serves both -- and inserts only the rows its own network evaluated; otherwise
+// the arena's own table.
+#ifdef SPMCTS_AB
+// SPMCTS_CACHE_SHARE=0 (A/B library): follower lanes keep a table of their own (the first form)
+static bool cache_share_off() {
+  static const bool v = getenv("SPMCTS_CACHE_SHARE") && strcmp(getenv("SPMCTS_CACHE_SHARE"), "0") == 0;
+  return v;
+}
+#else
+static constexpr bool cache_share_off() { return false; }
+#endif
+
+static bool cache_view(const spmcts_arena *h, View &v) {
+  v.cshared = 0;
+  const spmcts_arena *p = h->peer;
+  if (cache_share_off()) return false;
+  if (!v.cwin || !p || p->v.cwin != v.cwin || !p->v.ctag) return false;
+  const int d = (int)(v.cgen - p->v.cgen);
+  if (d < -1 || d > 1) return false;
+  v.ctag = p->v.ctag;
+  v.ckey = p->v.ckey;
+  v.cout = p->v.cout;
+  v.cmask = p->v.cmask;
+  v.cshared = 1;
+  return true;
+}
 
 static int geometry(const spmcts_config *c, int *A, int *P, int *cells, int *maxd, int *maxm) {
   if (c->game == SPMCTS_CONNECT4 && c->width == 7 && c->height == 6) {
@@ -2786,7 +2836,8 @@ int spmcts_arena_create(const spmcts_config *cfg, int device, spmcts_arena **out
     return rc;
   }
 #ifndef SPMCTS_AB
-  for (const char *n : {"SPMCTS_TREE_BLOCK", "SPMCTS_EXPAND_CO", "SPMCTS_TREE_COPIES", "SPMCTS_PEER_PUSH"})
+  for (const char *n : {"SPMCTS_TREE_BLOCK", "SPMCTS_EXPAND_CO", "SPMCTS_TREE_COPIES", "SPMCTS_PEER_PUSH",
+                        "SPMCTS_CACHE_SHARE"})
     if (getenv(n)) {
       delete h;
       return fail(SPMCTS_ERR_AB_SWITCH, std::string(n) + " is a switch of the A/B library (make ab: libspmcts_ab.so)");
@@ -2994,6 +3045,8 @@ static int launch_rows(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_de
   // the evaluation cache is live in leaf-dedup launches of single-network arenas (spmcts_set_eval_cache)
   h->cache_step = v.cwin > 0 && v.dedup && v.seg1 >= v.NS;
   if (!h->cache_step) v.cwin = 0;
+  h->cache_shared_step = h->cache_step && cache_view(h, v);
+  h->cache_tab = h->cache_step ? v.ctag : nullptr;
   v.served = h->cache_step ? 1 : 0;
   if (v.dedup) {
     if (++h->v.dgen == 0) ++h->v.dgen;  // generation 0 = the zeroed table
@@ -3091,7 +3144,10 @@ int spmcts_expand2(spmcts_arena *h, const float *probs0_dev, const float *values
   if (h->v.seg1 < h->v.NS && (!probs1_dev || !values1_dev))
     return fail(-1, "two-network arena needs network-1 outputs");
   if (h->cache_step) {  // the rows of this step consulted the evaluation cache: fills and inserts first
-    DISPATCH(h, hipLaunchKernelGGL(k_cache_io<GG>, dim3(nblk(h->v.NS, 256)), dim3(256), 0, (hipStream_t)stream, h->v,
+    View v = h->v;
+    if (h->cache_shared_step) cache_view(h, v);
+    if (v.ctag != h->cache_tab) return fail(-4, "the evaluation cache table changed between a step's rows and its expand");
+    DISPATCH(h, hipLaunchKernelGGL(k_cache_io<GG>, dim3(nblk(h->v.NS, 256)), dim3(256), 0, (hipStream_t)stream, v,
                                    (float *)probs0_dev, (float *)values0_dev));
     h->cache_step = false;
   }
@@ -3205,6 +3261,10 @@ int spmcts_set_eval_cache(spmcts_arena *h, int32_t window, int32_t capacity_log2
   if (!h) return fail(-1, "null arena");
   if (window < 0 || window > (1 << 20)) return fail(-3, "eval cache window out of range");
   if (capacity_log2 != 0 && (capacity_log2 < 10 || capacity_log2 > 28)) return fail(-3, "eval cache capacity_log2: 10..28 (0 = sized from the arena)");
+  if (h->cache_step) return fail(-4, "a step that consulted the evaluation cache has not been expanded yet");
+  for (const spmcts_arena *f : h->followers)
+    if (f->cache_step && f->cache_shared_step)
+      return fail(-4, "a follower lane's step that uses this arena's evaluation cache has not been expanded yet");
   HIP_TRY(hipSetDevice(h->device));
   HIP_TRY(hipDeviceSynchronize());  // no launch of this arena reads the old table any more
   for (void *p : h->cache_allocs) (void)hipFree(p);
@@ -3215,17 +3275,18 @@ int spmcts_set_eval_cache(spmcts_arena *h, int32_t window, int32_t capacity_log2
   v.xc = nullptr;
   v.cwin = 0;
   v.cmask = 0;
-  h->cache_step = false;
+  h->cache_step = h->cache_shared_step = false;
   if (window == 0) return 0;
   if (v.K < 2) return fail(-3, "the evaluation cache needs search_threads > 1 (it extends leaf dedup)");
   int L = capacity_log2;
   if (L == 0) {
-    // entries live in one window: at most one row per searching tree per sim, plus the end-of-ply rows;
-    // twice that, so probe chains stay short
+    // entries held: window + 1 generations (the slack one) of at most one row per searching tree per sim, plus
+    // the end-of-ply rows; a leader's table also takes a follower lane's rows (cache_view): twice one lane's, and
+    // twice that again so probe chains stay short
     const long long searching = std::max<long long>(v.G > 0 ? v.G : v.T, 1);
-    const long long live = (long long)window * searching * ((long long)v.iters + 2);
+    const long long held = (long long)(window + 1) * searching * ((long long)v.iters + 2);
     L = 10;
-    while (L < 26 && (1ll << L) < 2 * live) ++L;
+    while (L < 27 && (1ll << L) < 4 * held) ++L;
   }
   const size_t E = (size_t)1 << L;
   void *p[4] = {};
