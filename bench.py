@@ -406,7 +406,7 @@ def main():
     kw = dict(iterations=args.sims, seed=1234 + rank, device=dev, bucket=args.bucket, opponent=opponent, dtype=tdt,
               evaluate=arena_mode, record=not arena_mode, search_threads=args.search_threads,
               blocks_per_tree=args.blocks_per_tree, leaf_dedup=False if args.no_leaf_dedup else None,
-              eval_cache=0 if (args.no_leaf_dedup or arena_mode or args.search_threads < 2) else args.eval_cache)
+              eval_cache=0 if (args.no_leaf_dedup or args.search_threads < 2) else args.eval_cache)
     if args.lanes > 1:
         lane_sizes = None
         share = args.lane0_share

@@ -214,13 +214,15 @@ int spmcts_set_leaf_peer(spmcts_arena *h, spmcts_arena *leader);
  * leader-served step without it fails (-4). */
 int spmcts_peer_push(spmcts_arena *h, float *probs_dev, float *values_dev, const float *leader_probs_dev,
                      const float *leader_values_dev, spmcts_stream stream, spmcts_stream leader_stream);
-/* Evaluation cache (round 6; search_threads > 1 with leaf dedup on, single-network arenas): the network
+/* Evaluation cache (round 6; search_threads > 1 with leaf dedup on): the network
  * outputs of the arena's own leaf rows are kept, keyed like leaf dedup ((own, opp) stones from the mover's
  * view), for `window` generations -- one generation per spmcts_games_begin_ply / spmcts_search_begin, so
  * window 1 = within the ply (search) that evaluated them.  An owner leaf whose key is cached takes a row
  * after the network rows (and a follower's leader-served rows) and, at spmcts_expand / spmcts_expand2, the
  * cached outputs are written into that row of probs / values (k_cache_io), and the rows the network (or the
- * leader) filled go into the cache.  The reference evaluates every leaf (inference_worker.py:89-119); with
+ * leader) filled go into the cache.  Two-network arenas keep the networks' keys apart (served rows follow each
+ * segment's network rows); a follower lane whose leader runs a cache of the same window uses the leader's
+ * table.  The reference evaluates every leaf (inference_worker.py:89-119); with
  * a deterministic, batch-independent evaluator every leaf still receives exactly its own outputs.  After the
  * network's weights change call spmcts_eval_cache_clear.  window 0 turns it off; capacity_log2 = log2 of the
  * table's entries (10..28; 0 = twice the rows one window can hold), allocated here (24 + 4 (A + 1) bytes

@@ -229,8 +229,9 @@ class Arena:
     def set_eval_cache(self, window, capacity_log2=0):
         """Evaluation cache (include/spmcts.h spmcts_set_eval_cache): a leaf whose network input this arena
         evaluated in the last `window` plies (searches) takes those outputs instead of a row of its own; 0 =
-        off.  Needs leaf dedup; single-network arenas (elsewhere it stays idle).  Same evaluator contract as
-        leaf dedup (pure, batch-independent); call eval_cache_clear() when the weights change."""
+        off.  Needs leaf dedup (idle without it).  Same evaluator contract as leaf dedup (pure,
+        batch-independent; the two networks of an evaluation arena keep separate keys); call eval_cache_clear()
+        when the weights change."""
         torch.cuda.current_stream().synchronize()
         call("spmcts_set_eval_cache", self.h, int(window), int(capacity_log2))
         self.eval_cache = int(window)

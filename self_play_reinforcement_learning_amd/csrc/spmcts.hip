@@ -1492,13 +1492,19 @@ __global__ __launch_bounds__(256) void k_peer_push(View v, const int32_t *psrow,
 // the leader fills) puts them in the cache under the current generation (nothing is cached when no entry
 // within CACHE_PROBES is free).  Duplicates (down 0) read their owner's row.
 template <class G>
-__global__ __launch_bounds__(256) void k_cache_io(View v, float *probs, float *values) {
+__global__ __launch_bounds__(256) void k_cache_io(View v, float *probs0, float *values0, float *probs1,
+                                                  float *values1) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= v.NS || !v.need[t]) return;
   const int d = v.down[t];
   if (d == 0) return;
-  const int r = v.srow[t], A = v.A;
-  float *pr = probs + (size_t)r * A;
+  const int A = v.A;
+  // network-1 rows (two-network arenas) live in their own output buffers, indexed by row - seg1
+  const int row = v.srow[t];
+  const bool n1 = row >= v.seg1;
+  const int r = n1 ? row - v.seg1 : row;
+  float *values = n1 ? values1 : values0;
+  float *pr = (n1 ? probs1 : probs0) + (size_t)r * A;
   if (d == 3) {
     const float *c = v.cout + (size_t)v.xc[t] * (A + 1);
     for (int a = 0; a < A; ++a) pr[a] = c[a];
@@ -1551,19 +1557,24 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_need(View v, int32_t *cou
   // wave totals of the two segments' owner counts (a two-level scan: 6 shuffle steps within each wave,
   // 3 over the 8 wave totals, 2 barriers; the round-3 1,024-entry Hillis-Steele scan took 20 barriers
   // and 8 KB of LDS)
-  __shared__ int32_t s_w0[SCAN_WAVES], s_w1[SCAN_WAVES], s_w2[SCAN_WAVES];
+  __shared__ int32_t s_w0[SCAN_WAVES], s_w1[SCAN_WAVES], s_w2[SCAN_WAVES], s_w4[SCAN_WAVES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T = v.NS;  // pending slots (tree * K + j), tree order then in-flight order
   const int chunk = (T + SCAN_THREADS - 1) / SCAN_THREADS;
   const int lo = min(T, tid * chunk), hi = min(T, lo + chunk);
-  int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+  // c0 / c1: network-0 / network-1 rows the networks evaluate; c2 / c4: served rows (leader- or cache-served) of
+  // network 0 / 1, numbered after the evaluated rows of their segment; c3: cache-served rows (a counter)
+  int c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0;
   // unrolled so each thread's chunk of flags is fetched in one round of independent loads
-  if (v.served) {  // single network: own rows, then the leader-served and cache-served rows
+  if (v.served) {
 #pragma unroll 16
     for (int t = lo; t < hi; ++t) {
       const int d = v.down[t];
-      c0 += d == 1;
-      c2 += d >= 2;
+      const bool n1 = v.tnet[t / v.K] != 0;
+      c0 += d == 1 && !n1;
+      c1 += d == 1 && n1;
+      c2 += d >= 2 && !n1;
+      c4 += d >= 2 && n1;
       c3 += d == 3;
     }
   } else {
@@ -1573,56 +1584,67 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_need(View v, int32_t *cou
         if (v.tnet[t / v.K]) ++c1; else ++c0;
       }
   }
-  // inclusive scans of (c0, c1, c2) in thread order: within the wave, then over the wave totals
-  int i0 = c0, i1 = c1, i2 = c2;
+  // inclusive scans of (c0, c1, c2, c4) in thread order: within the wave, then over the wave totals
+  int i0 = c0, i1 = c1, i2 = c2, i4 = c4;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
     const int a0 = __shfl_up(i0, off, 64), a1 = __shfl_up(i1, off, 64), a2 = __shfl_up(i2, off, 64);
+    const int a4 = __shfl_up(i4, off, 64);
     if (lane >= off) {
       i0 += a0;
       i1 += a1;
       i2 += a2;
+      i4 += a4;
     }
   }
   if (lane == 63) {
     s_w0[wave] = i0;
     s_w1[wave] = i1;
     s_w2[wave] = i2;
+    s_w4[wave] = i4;
   }
   __syncthreads();
   if (wave == 0) {
     int w0 = lane < SCAN_WAVES ? s_w0[lane] : 0, w1 = lane < SCAN_WAVES ? s_w1[lane] : 0;
-    int w2 = lane < SCAN_WAVES ? s_w2[lane] : 0;
+    int w2 = lane < SCAN_WAVES ? s_w2[lane] : 0, w4 = lane < SCAN_WAVES ? s_w4[lane] : 0;
 #pragma unroll
     for (int off = 1; off < SCAN_WAVES; off <<= 1) {
       const int a0 = __shfl_up(w0, off, 64), a1 = __shfl_up(w1, off, 64), a2 = __shfl_up(w2, off, 64);
+      const int a4 = __shfl_up(w4, off, 64);
       if (lane >= off) {
         w0 += a0;
         w1 += a1;
         w2 += a2;
+        w4 += a4;
       }
     }
     if (lane < SCAN_WAVES) {
       s_w0[lane] = w0;
       s_w1[lane] = w1;
       s_w2[lane] = w2;
+      s_w4[lane] = w4;
     }
   }
   __syncthreads();
   i0 += wave ? s_w0[wave - 1] : 0;
   i1 += wave ? s_w1[wave - 1] : 0;
   i2 += wave ? s_w2[wave - 1] : 0;
+  i4 += wave ? s_w4[wave - 1] : 0;
   int r0 = i0 - c0, r1 = v.seg1 + i1 - c1;
   if (v.served) {
-    int r2 = s_w0[SCAN_WAVES - 1] + i2 - c2;  // the leader- and cache-served rows follow all own rows
+    // served rows follow all evaluated rows of their network's segment
+    int r2 = s_w0[SCAN_WAVES - 1] + i2 - c2, r4 = v.seg1 + s_w1[SCAN_WAVES - 1] + i4 - c4;
 #pragma unroll 16
     for (int t = lo; t < hi; ++t) {
       const int d = v.down[t];
+      if (d == 0) continue;
+      const bool n1 = v.tnet[t / v.K] != 0;
       if (d == 1) {
-        v.row_tree[r0] = t;
-        v.srow[t] = r0++;
-      } else if (d >= 2) {
-        v.srow[t] = r2++;
+        const int r = n1 ? r1++ : r0++;
+        v.row_tree[r] = t;
+        v.srow[t] = r;
+      } else {
+        v.srow[t] = n1 ? r4++ : r2++;
       }
     }
     if (v.cwin) {  // cache-served rows (counters.cache_rows)
@@ -3042,8 +3064,8 @@ static int launch_rows(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_de
     }
   View v = h->v;
   v.peer_on = 0;
-  // the evaluation cache is live in leaf-dedup launches of single-network arenas (spmcts_set_eval_cache)
-  h->cache_step = v.cwin > 0 && v.dedup && v.seg1 >= v.NS;
+  // the evaluation cache is live in leaf-dedup launches (spmcts_set_eval_cache)
+  h->cache_step = v.cwin > 0 && v.dedup;
   if (!h->cache_step) v.cwin = 0;
   h->cache_shared_step = h->cache_step && cache_view(h, v);
   h->cache_tab = h->cache_step ? v.ctag : nullptr;
@@ -3148,7 +3170,8 @@ int spmcts_expand2(spmcts_arena *h, const float *probs0_dev, const float *values
     if (h->cache_shared_step) cache_view(h, v);
     if (v.ctag != h->cache_tab) return fail(-4, "the evaluation cache table changed between a step's rows and its expand");
     DISPATCH(h, hipLaunchKernelGGL(k_cache_io<GG>, dim3(nblk(h->v.NS, 256)), dim3(256), 0, (hipStream_t)stream, v,
-                                   (float *)probs0_dev, (float *)values0_dev));
+                                   (float *)probs0_dev, (float *)values0_dev, (float *)probs1_dev,
+                                   (float *)values1_dev));
     h->cache_step = false;
   }
   const int gpb = 64 / h->P;

@@ -95,8 +95,8 @@ class SelfPlayEngine:
         selfplayworker.py:71-81); None = the policy's.  dtype: the fused trunk's element type, fp16 by
         default (the reference's inference autocast, inference_worker.py:114-119) or bf16.  eval_cache: plies
         a position's network outputs stay cached (include/spmcts.h spmcts_set_eval_cache; 0 = off, 1 = within
-        the ply that evaluated them); needs leaf dedup (a pure evaluator, search_threads > 1) and one network;
-        None = 1 where those hold, else 0."""
+        the ply that evaluated them); needs leaf dedup (pure evaluators, search_threads > 1); None = 1 where
+        that holds, else 0."""
         self.game = game
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.evaluator = make_evaluator(network, game, device=self.device, dtype=dtype, leaf_layout=leaf_layout)
@@ -159,10 +159,10 @@ class SelfPlayEngine:
         if self.leaf_dedup:
             self.arena.set_leaf_dedup(True)
         # evaluation cache (include/spmcts.h spmcts_set_eval_cache): the dedup key extended over plies
-        cache_ok = self.leaf_dedup and self.evaluator1 is None
+        cache_ok = self.leaf_dedup  # pure evaluators (both networks of an evaluation arena: keys carry the network)
         self.eval_cache = (1 if cache_ok else 0) if eval_cache is None else int(eval_cache)
         if self.eval_cache and not cache_ok:
-            raise ValueError("eval_cache needs leaf dedup (a pure evaluator, search_threads > 1) and a single network")
+            raise ValueError("eval_cache needs leaf dedup (pure evaluators, search_threads > 1)")
         if self.eval_cache:
             self.arena.set_eval_cache(self.eval_cache)
         self.n_games = n_games

@@ -878,6 +878,32 @@ def test_eval_cache_with_cross_lane_dedup_is_exact(lanes, sizes):
           f"{c2['nn_rows'] / c2['nn_leaves']:.4f}")
 
 
+def test_eval_cache_two_networks_exact():
+    """Evaluation arena (policy vs a second network, evaluate mode, rows in two segments): the cache keeps the two
+    networks' keys apart and serves each segment's rows after its network rows; results and counters equal those of
+    per-step dedup alone, with fewer network rows."""
+    from self_play_reinforcement_learning_amd.engine import SelfPlayEngine
+    from self_play_reinforcement_learning_amd.modules import ResidualTower
+
+    torch.manual_seed(0)
+    net = ResidualTower(7, 6, 7, num_blocks=2, filter_factor=32)
+    torch.manual_seed(1)
+    opp = ResidualTower(7, 6, 7, num_blocks=2, filter_factor=32)
+    out = []
+    for w in (0, 2):
+        eng = SelfPlayEngine("connect4", net, n_games=256, iterations=12, seed=5, max_games=512, opponent=opp,
+                             evaluate=True, search_threads=4, eval_cache=w, record=False)
+        assert eng.eval_cache == w and eng.evaluator1 is not None
+        eng.run(games=512)
+        eng.check()
+        out.append(eng.counters())
+    c0, c1 = out
+    for k in ("sims", "leaked_sims", "moves", "nn_leaves", "terminal_leaves", "depth_sum", "games_finished", "results"):
+        assert c0[k] == c1[k], k
+    assert c1["cache_rows"] > 0 and c1["nn_rows"] + c1["cache_rows"] == c0["nn_rows"]
+    print(f"eval cache, two networks: rows/leaf {c0['nn_rows'] / c0['nn_leaves']:.4f} -> {c1['nn_rows'] / c1['nn_leaves']:.4f}")
+
+
 def test_eval_cache_cleared_on_new_weights():
     """refresh_network after the weights change clears the cache (spmcts_eval_cache_clear): the plies after the
     change see the new network's outputs only, exactly as the run without a cache does."""
@@ -909,7 +935,7 @@ def test_eval_cache_cleared_on_new_weights():
 
 def test_eval_cache_rules():
     """spmcts_set_eval_cache refuses what it cannot serve exactly: search_threads 1 (no dedup rows) and a bad
-    capacity; SelfPlayEngine refuses it without leaf dedup or with two networks."""
+    capacity; SelfPlayEngine refuses it without leaf dedup."""
     from self_play_reinforcement_learning_amd import _lib
     from self_play_reinforcement_learning_amd.arena import Arena
     from self_play_reinforcement_learning_amd.engine import SelfPlayEngine
@@ -930,11 +956,6 @@ def test_eval_cache_rules():
     net = ResidualTower(7, 6, 7, num_blocks=2, filter_factor=32)
     with pytest.raises(ValueError, match="eval_cache"):
         SelfPlayEngine("connect4", net, n_games=64, iterations=8, search_threads=4, leaf_dedup=False, eval_cache=1)
-    torch.manual_seed(1)
-    opp = ResidualTower(7, 6, 7, num_blocks=2, filter_factor=32)
-    with pytest.raises(ValueError, match="eval_cache"):
-        SelfPlayEngine("connect4", net, n_games=64, iterations=8, search_threads=4, opponent=opp, evaluate=True,
-                       eval_cache=1)
 
 
 def test_bench_line_small_with_no_dedup_twin():
