@@ -680,7 +680,8 @@ def main():
     out["cpu_baseline"] = cpu
 
     def twin(plies):
-        """`plies` more plies on the same arenas right after the timed region: (positions/s, ms per ply, rows per leaf)."""
+        """`plies` more plies on the same arenas right after the timed region: (the headline's unit per second --
+        positions/s, games/s in arena mode --, ms per ply, rows per leaf)."""
         eng.check()
         t_c0 = eng.counters()
         D.barrier()
@@ -695,7 +696,8 @@ def main():
         t_el = D.all_reduce_max(time.perf_counter() - t_t0)
         t_c1 = eng.counters()
         eng.check()
-        t_moves = int(D.all_reduce_stats([t_c1["moves"] - t_c0["moves"]])[0])
+        unit = "games_finished" if arena_mode else "moves"
+        t_moves = int(D.all_reduce_stats([t_c1[unit] - t_c0[unit]])[0])
         return (t_moves / t_el, t_el / plies * 1e3,
                 (t_c1["nn_rows"] - t_c0["nn_rows"]) / max(1, t_c1["nn_leaves"] - t_c0["nn_leaves"]))
 
