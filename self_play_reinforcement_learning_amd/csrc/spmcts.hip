@@ -1565,12 +1565,13 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_need(View v, int32_t *cou
   // c0 / c1: network-0 / network-1 rows the networks evaluate; c2 / c4: served rows (leader- or cache-served) of
   // network 0 / 1, numbered after the evaluated rows of their segment; c3: cache-served rows (a counter)
   int c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0;
+  const bool two = v.seg1 < v.NS;  // two-network arena (single-network: no tnet loads)
   // unrolled so each thread's chunk of flags is fetched in one round of independent loads
   if (v.served) {
 #pragma unroll 16
     for (int t = lo; t < hi; ++t) {
       const int d = v.down[t];
-      const bool n1 = v.tnet[t / v.K] != 0;
+      const bool n1 = two && v.tnet[t / v.K] != 0;
       c0 += d == 1 && !n1;
       c1 += d == 1 && n1;
       c2 += d >= 2 && !n1;
@@ -1638,7 +1639,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_need(View v, int32_t *cou
     for (int t = lo; t < hi; ++t) {
       const int d = v.down[t];
       if (d == 0) continue;
-      const bool n1 = v.tnet[t / v.K] != 0;
+      const bool n1 = two && v.tnet[t / v.K] != 0;
       if (d == 1) {
         const int r = n1 ? r1++ : r0++;
         v.row_tree[r] = t;
