@@ -225,8 +225,8 @@ int spmcts_peer_push(spmcts_arena *h, float *probs_dev, float *values_dev, const
  * table.  The reference evaluates every leaf (inference_worker.py:89-119); with
  * a deterministic, batch-independent evaluator every leaf still receives exactly its own outputs.  After the
  * network's weights change call spmcts_eval_cache_clear.  window 0 turns it off; capacity_log2 = log2 of the
- * table's entries (10..28; 0 = twice the rows one window can hold), allocated here (24 + 4 (A + 1) bytes
- * per entry + 4 per pending slot, outside spmcts_arena_bytes).  (sync) */
+ * table's entries (10..28; 0 = four times the rows window + 1 plies can hold, at most 2^26), allocated here
+ * (one 64-byte record per entry + 4 bytes per pending slot, outside spmcts_arena_bytes).  (sync) */
 int spmcts_set_eval_cache(spmcts_arena *h, int32_t window, int32_t capacity_log2);
 /* Every cached output leaves the window (host-side generation step; no device work). */
 int spmcts_eval_cache_clear(spmcts_arena *h);

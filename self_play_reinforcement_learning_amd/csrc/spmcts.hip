@@ -131,9 +131,9 @@ struct View {
   // evaluation cache (round 6, spmcts_set_eval_cache): network outputs of the arena's own rows kept for `cwin`
   // generations (one per ply / search), keyed like the dedup table; an owner slot whose key is there takes
   // the cached outputs (down 3, xc = the entry) in a row after the network rows, filled by k_cache_io.
-  // ctag: (generation << 32 | 1) per entry, 0 = never used; ckey: 2 x u64; cout: A probs + value
-  uint64_t *ctag, *ckey;
-  float *cout;
+  // crec: one 64-byte record per entry (one line per probe): tag u64 ((generation << 32) | state, 0 = never used),
+  // own u64, opp u64, then A probs + value as f32
+  uint64_t *crec;
   int32_t *xc;
   int cwin, cmask;  // cwin 0 = off (also in launches where the cache is not live)
   uint32_t cgen;
@@ -1383,8 +1383,14 @@ __global__ __launch_bounds__(256) void k_dedup_insert(View v) {
 constexpr int CACHE_PROBES = 32;
 constexpr unsigned long long CACHE_READY = 1ull, CACHE_BUSY = 2ull;
 
-__device__ __forceinline__ unsigned long long cache_tag_load(const View &v, uint32_t h) {
-  return __hip_atomic_load((unsigned long long *)v.ctag + h, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+constexpr int CACHE_REC = 8;  // u64 words per record (64 bytes): tag, own, opp, (A + 1) f32 (A <= 9)
+static_assert(24 + 4 * (C4::A + 1) <= 8 * CACHE_REC && 24 + 4 * (TTT::A + 1) <= 8 * CACHE_REC, "cache record");
+
+__device__ __forceinline__ unsigned long long *cache_rec(const View &v, uint32_t h) {
+  return (unsigned long long *)v.crec + (size_t)h * CACHE_REC;
+}
+__device__ __forceinline__ float *cache_out(const View &v, uint32_t h) {
+  return (float *)(cache_rec(v, h) + 3);
 }
 
 __device__ __forceinline__ bool cache_live_tag(const View &v, unsigned long long tag) {
@@ -1397,12 +1403,23 @@ __device__ __forceinline__ bool cache_free_tag(const View &v, unsigned long long
   return tag == 0 || ((tag & 0xffffffffull) == CACHE_READY && d > v.cwin);
 }
 
+// The probe loop reads records with plain loads (a stale line only makes a miss or an early stop: the position
+// is then evaluated); a candidate is confirmed after an acquire fence by atomic re-reads of its tag and key, so a
+// hit is a READY record whose key and outputs were published before the tag.
 __device__ __forceinline__ int cache_find(const View &v, uint64_t own, uint64_t opp) {
   uint32_t h = leaf_hash(own, opp) & (uint32_t)v.cmask;
   for (int p = 0; p < CACHE_PROBES; ++p) {
-    const unsigned long long tag = cache_tag_load(v, h);
+    const unsigned long long *r = cache_rec(v, h);
+    const unsigned long long tag = r[0];
     if (tag == 0) return -1;
-    if (cache_live_tag(v, tag) && v.ckey[2 * (size_t)h] == own && v.ckey[2 * (size_t)h + 1] == opp) return (int)h;
+    if (cache_live_tag(v, tag) && r[1] == own && r[2] == opp) {
+      __atomic_thread_fence(__ATOMIC_ACQUIRE);
+      unsigned long long *rw = cache_rec(v, h);
+      const unsigned long long t2 = __hip_atomic_load(rw, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long o2 = __hip_atomic_load(rw + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long q2 = __hip_atomic_load(rw + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return cache_live_tag(v, t2) && o2 == own && q2 == opp ? (int)h : -1;
+    }
     h = (h + 1) & (uint32_t)v.cmask;
   }
   return -1;
@@ -1415,8 +1432,8 @@ __device__ __forceinline__ bool cache_hit(const View &v, int t) {
   leaf_key<G>(v, t, own, opp);
   const int e = cache_find(v, own, opp);
   if (e < 0) return false;
-  __hip_atomic_store((unsigned long long *)v.ctag + e, ((unsigned long long)v.cgen << 32) | CACHE_READY,
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(cache_rec(v, e), ((unsigned long long)v.cgen << 32) | CACHE_READY, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
   v.xc[t] = e;
   return true;
 }
@@ -1506,7 +1523,7 @@ __global__ __launch_bounds__(256) void k_cache_io(View v, float *probs0, float *
   float *values = n1 ? values1 : values0;
   float *pr = (n1 ? probs1 : probs0) + (size_t)r * A;
   if (d == 3) {
-    const float *c = v.cout + (size_t)v.xc[t] * (A + 1);
+    const float *c = cache_out(v, v.xc[t]);
     for (int a = 0; a < A; ++a) pr[a] = c[a];
     values[r] = c[A];
     return;
@@ -1516,18 +1533,18 @@ __global__ __launch_bounds__(256) void k_cache_io(View v, float *probs0, float *
   leaf_key<G>(v, t, own, opp);
   uint32_t h = leaf_hash(own, opp) & (uint32_t)v.cmask;
   const unsigned long long gen = (unsigned long long)v.cgen << 32;
-  unsigned long long *tag = (unsigned long long *)v.ctag;
   for (int p = 0; p < CACHE_PROBES; ++p) {
-    unsigned long long w = cache_tag_load(v, h);
+    unsigned long long *rec = cache_rec(v, h);
+    unsigned long long w = __hip_atomic_load(rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     while (cache_free_tag(v, w)) {  // never used, or behind the window (+1): free to take
-      const unsigned long long old = atomicCAS(tag + h, w, gen | CACHE_BUSY);
+      const unsigned long long old = atomicCAS(rec, w, gen | CACHE_BUSY);
       if (old == w) {
-        v.ckey[2 * (size_t)h] = own;
-        v.ckey[2 * (size_t)h + 1] = opp;
-        float *c = v.cout + (size_t)h * (A + 1);
+        rec[1] = own;
+        rec[2] = opp;
+        float *c = cache_out(v, h);
         for (int a = 0; a < A; ++a) c[a] = pr[a];
         c[A] = values[r];
-        __hip_atomic_store(tag + h, gen | CACHE_READY, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(rec, gen | CACHE_READY, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }
       w = old;  // another insert took it first: probe on
@@ -2594,12 +2611,10 @@ static bool cache_view(const spmcts_arena *h, View &v) {
   v.cshared = 0;
   const spmcts_arena *p = h->peer;
   if (cache_share_off()) return false;
-  if (!v.cwin || !p || p->v.cwin != v.cwin || !p->v.ctag) return false;
+  if (!v.cwin || !p || p->v.cwin != v.cwin || !p->v.crec) return false;
   const int d = (int)(v.cgen - p->v.cgen);
   if (d < -1 || d > 1) return false;
-  v.ctag = p->v.ctag;
-  v.ckey = p->v.ckey;
-  v.cout = p->v.cout;
+  v.crec = p->v.crec;
   v.cmask = p->v.cmask;
   v.cshared = 1;
   return true;
@@ -3069,7 +3084,7 @@ static int launch_rows(spmcts_arena *h, void *leaves_dev, int32_t *leaf_count_de
   h->cache_step = v.cwin > 0 && v.dedup;
   if (!h->cache_step) v.cwin = 0;
   h->cache_shared_step = h->cache_step && cache_view(h, v);
-  h->cache_tab = h->cache_step ? v.ctag : nullptr;
+  h->cache_tab = h->cache_step ? v.crec : nullptr;
   v.served = h->cache_step ? 1 : 0;
   if (v.dedup) {
     if (++h->v.dgen == 0) ++h->v.dgen;  // generation 0 = the zeroed table
@@ -3169,7 +3184,7 @@ int spmcts_expand2(spmcts_arena *h, const float *probs0_dev, const float *values
   if (h->cache_step) {  // the rows of this step consulted the evaluation cache: fills and inserts first
     View v = h->v;
     if (h->cache_shared_step) cache_view(h, v);
-    if (v.ctag != h->cache_tab) return fail(-4, "the evaluation cache table changed between a step's rows and its expand");
+    if (v.crec != h->cache_tab) return fail(-4, "the evaluation cache table changed between a step's rows and its expand");
     DISPATCH(h, hipLaunchKernelGGL(k_cache_io<GG>, dim3(nblk(h->v.NS, 256)), dim3(256), 0, (hipStream_t)stream, v,
                                    (float *)probs0_dev, (float *)values0_dev, (float *)probs1_dev,
                                    (float *)values1_dev));
@@ -3294,8 +3309,7 @@ int spmcts_set_eval_cache(spmcts_arena *h, int32_t window, int32_t capacity_log2
   for (void *p : h->cache_allocs) (void)hipFree(p);
   h->cache_allocs.clear();
   View &v = h->v;
-  v.ctag = v.ckey = nullptr;
-  v.cout = nullptr;
+  v.crec = nullptr;
   v.xc = nullptr;
   v.cwin = 0;
   v.cmask = 0;
@@ -3310,12 +3324,12 @@ int spmcts_set_eval_cache(spmcts_arena *h, int32_t window, int32_t capacity_log2
     const long long searching = std::max<long long>(v.G > 0 ? v.G : v.T, 1);
     const long long held = (long long)(window + 1) * searching * ((long long)v.iters + 2);
     L = 10;
-    while (L < 27 && (1ll << L) < 4 * held) ++L;
+    while (L < 26 && (1ll << L) < 4 * held) ++L;
   }
   const size_t E = (size_t)1 << L;
-  void *p[4] = {};
-  const size_t bytes[4] = {E * 8, E * 16, E * sizeof(float) * (h->A + 1), (size_t)v.NS * 4};
-  for (int i = 0; i < 4; ++i) {
+  void *p[2] = {};
+  const size_t bytes[2] = {E * CACHE_REC * 8, (size_t)v.NS * 4};
+  for (int i = 0; i < 2; ++i) {
     const hipError_t e = hipMalloc(&p[i], bytes[i]);
     if (e != hipSuccess) {
       for (int j = 0; j < i; ++j) (void)hipFree(p[j]);
@@ -3324,10 +3338,8 @@ int spmcts_set_eval_cache(spmcts_arena *h, int32_t window, int32_t capacity_log2
     h->cache_allocs.push_back(p[i]);
   }
   HIP_TRY(hipMemset(p[0], 0, bytes[0]));  // every entry never used
-  v.ctag = (uint64_t *)p[0];
-  v.ckey = (uint64_t *)p[1];
-  v.cout = (float *)p[2];
-  v.xc = (int32_t *)p[3];
+  v.crec = (uint64_t *)p[0];
+  v.xc = (int32_t *)p[1];
   v.cmask = (int)(E - 1);
   v.cwin = window;
   v.cgen = (uint32_t)window + 1;  // generation 0 never read as live
