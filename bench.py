@@ -597,6 +597,7 @@ def main():
             "traffic_source": traffic_src,
             "flops_per_launch": tw_flops_per_launch,
             "flops_per_leaf": trunk_fpl,
+            "rows_per_launch": rows / max(1, tw_launches),
             "avg_launch_us": tw_avg_s * 1e6,
             "launches": tw_launches,
             "lanes": lanes,
