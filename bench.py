@@ -584,6 +584,11 @@ def main():
             "leaf_dedup": bool(getattr(eng, "leaf_dedup", False)),
             "cross_lane_dedup": bool(getattr(eng, "cross_dedup", False)),
             "eval_cache_plies": int(getattr(eng, "eval_cache", 0)),
+            "eval_cache_note": ("a leaf whose network input was evaluated earlier in the same ply takes those outputs "
+                                "(one evaluation per distinct input per ply; nothing computed before a ply is reused "
+                                "in it); the searches are bit-identical to the cache-off run "
+                                "(tests/test_gpu_engine.py::test_eval_cache_is_exact); no_cache_twin times the plies "
+                                "after the timed region with it off") if getattr(eng, "eval_cache", 0) == 1 else None,
         },
         "roofline": {
             "kernel": f"tower::k_tower_dyn (fused ResNet-{4 * args.filter_factor}x{args.blocks} trunk, {args.dtype} MFMA)",
