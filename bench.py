@@ -713,7 +713,7 @@ def main():
             e.eval_cache = 0
         v_, ms_, rpl_ = twin(args.twin_no_cache)
         out["no_cache_twin"] = {
-            "plies": args.twin_no_cache, "value": v_, "ms_per_step": ms_, "rows_per_leaf": rpl_,
+            "plies": args.twin_no_cache, "value": v_, "unit": out["unit"], "ms_per_step": ms_, "rows_per_leaf": rpl_,
             "note": "the plies right after the timed region, evaluation cache off (spmcts_set_eval_cache 0): leaf "
                     "dedup within each simulation step only"}
     if args.twin_no_dedup > 0 and getattr(eng, "leaf_dedup", False):
@@ -724,7 +724,7 @@ def main():
         eng.leaf_dedup = False
         v_, ms_, rpl_ = twin(args.twin_no_dedup)
         out["no_dedup_twin"] = {
-            "plies": args.twin_no_dedup, "value": v_, "ms_per_step": ms_, "rows_per_leaf": rpl_,
+            "plies": args.twin_no_dedup, "value": v_, "unit": out["unit"], "ms_per_step": ms_, "rows_per_leaf": rpl_,
             "note": "the plies right after the timed region, leaf dedup off (spmcts_set_leaf_dedup): every leaf "
                     "evaluated in its own row, as the reference's InferenceWorker"}
     if args.secondary and not arena_mode:

@@ -1007,3 +1007,22 @@ def test_bench_line_small_with_eval_cache():
     tw, td = d["no_cache_twin"], d["no_dedup_twin"]
     assert tw["plies"] == 2 and tw["value"] > 0 and d["nn"]["rows_per_leaf"] < tw["rows_per_leaf"] < 1.0
     assert td["rows_per_leaf"] == 1.0
+
+
+def test_bench_arena_line_with_eval_cache():
+    """bench.py --mode arena (two networks, evaluate mode) runs the evaluation cache by default; its twins report
+    the headline's unit (games/s)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--mode", "arena", "--games", "256", "--sims", "16",
+           "--blocks", "2", "--steps", "6", "--warmup", "6", "--no-cpu-baseline", "--twin-no-cache", "4",
+           "--twin-no-dedup", "0"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=root, check=True).stdout
+    d = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
+    assert d["unit"] == "games/s" and d["config"]["eval_cache_plies"] == 1 and d["nn"]["cache_rows"] > 0
+    tw = d["no_cache_twin"]
+    assert tw["unit"] == "games/s" and tw["value"] >= 0 and d["nn"]["rows_per_leaf"] < tw["rows_per_leaf"] <= 1.0
