@@ -380,6 +380,44 @@ class Arena:
         f = self._finish.cpu()
         return int(f[0]), int(f[1])
 
+    def finish_export_async(self, refill=True):
+        """games_finish_ply + export_moves of the whole export ring without a host synchronisation: the records go
+        to persistent buffers of the ring's capacity and the counts to pinned host memory; returns an event for
+        finish_export_result.  Several lanes can queue theirs before the host waits on any of them."""
+        if getattr(self, "_exp", None) is None:
+            cap = max(64, 4 * self.n_games * ((self.cells + 1) // 2 + 1))  # spmcts.hip plan_arena: ex_cap (MAXM)
+            dev = self.device
+            self._exp = dict(
+                state=torch.empty((cap, self.cells), dtype=torch.int8, device=dev),
+                tree_probs=torch.empty((cap, self.A), dtype=torch.float32, device=dev),
+                q=torch.empty(cap, dtype=torch.float64, device=dev),
+                q_f64=torch.empty(cap, dtype=torch.uint8, device=dev),
+                z=torch.empty(cap, dtype=torch.float32, device=dev),
+                game=torch.empty(cap, dtype=torch.int64, device=dev),
+            )
+            self._exp_cap = cap
+            self._exp_count = torch.zeros(4, dtype=torch.int32, device=dev)
+            self._exp_host = torch.zeros(3, dtype=torch.int32).pin_memory()
+        e = self._exp
+        call("spmcts_games_finish_ply", self.h, int(bool(refill)), ptr(self._finish), _stream())
+        call("spmcts_export_moves", self.h, ptr(e["state"]), ptr(e["tree_probs"]), ptr(e["q"]), ptr(e["q_f64"]),
+             ptr(e["z"]), ptr(e["game"]), self._exp_cap, ptr(self._exp_count), _stream())
+        self._exp_host[0:2].copy_(self._finish, non_blocking=True)
+        self._exp_host[2:3].copy_(self._exp_count[0:1], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return ev
+
+    def finish_export_result(self, ev):
+        """(#games finished, Move records) of finish_export_async once `ev` has completed (waits for it); the
+        records are copies (queued on the current stream), so the persistent buffers can be reused next ply."""
+        ev.synchronize()
+        finished, ring, k = (int(x) for x in self._exp_host.tolist())
+        if k != ring:
+            raise _lib.SpmctsError(f"Move export took {k} of {ring} ring records (buffer capacity {self._exp_cap})")
+        moves = {key: v[:k].clone() for key, v in self._exp.items()} if k else None
+        return finished, moves
+
     def export_moves(self, max_records):
         dev = self.device
         n = max(1, int(max_records))

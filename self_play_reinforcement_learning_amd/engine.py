@@ -353,11 +353,17 @@ class SelfPlayEngine:
         return self._ply_finish(on_moves, refill, game_offset)
 
     def _ply_finish(self, on_moves=None, refill=True, game_offset=0):
-        a = self.arena
-        finished, ring = a.games_finish_ply(refill=refill)
+        return self._ply_finish_result(self._ply_finish_async(refill), on_moves, game_offset)
+
+    def _ply_finish_async(self, refill=True):
+        """The ply's results and Move export queued on the current stream (Arena.finish_export_async)."""
+        return self.arena.finish_export_async(refill=refill)
+
+    def _ply_finish_result(self, ev, on_moves=None, game_offset=0):
+        """Wait for _ply_finish_async's event, hand the Moves on, count them."""
+        finished, moves = self.arena.finish_export_result(ev)
         exported = 0
-        if ring:
-            moves = a.export_moves(ring)
+        if moves is not None:
             if game_offset:
                 moves["game"] += game_offset
             exported = int(moves["z"].shape[0])
@@ -704,10 +710,12 @@ class LanedEngine:
                 self._each(lambda e: e._peer_push())
                 self._each(lambda e: e._expand_dev(sim=True))
             self._each(lambda e: e._ply_move())
+            # every lane's results and export queued before the host waits on any of them (one round trip)
+            evs = self._each(lambda e: e._ply_finish_async(refill))
             res = []
-            for i, (e, st) in enumerate(zip(self.lanes, self.streams)):
+            for i, (e, st, ev) in enumerate(zip(self.lanes, self.streams, evs)):
                 with self._stream(st):  # on_moves runs on the lane's stream, after its export
-                    res.append(e._ply_finish(on_moves, refill, game_offset=i * self.GAME_ID_STRIDE))
+                    res.append(e._ply_finish_result(ev, on_moves, game_offset=i * self.GAME_ID_STRIDE))
         self._caller_waits_lanes()
         return sum(r[0] for r in res), sum(r[1] for r in res)
 

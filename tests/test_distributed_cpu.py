@@ -186,6 +186,13 @@ class _FakeLane(_FakeEngine):
     def _ply_move(self):
         assert self.sims == self.iterations
 
+    def _ply_finish_async(self, refill=True):  # LanedEngine queues every lane's finish before reading any
+        return ("finish", self.plies_run)
+
+    def _ply_finish_result(self, ev, on_moves=None, game_offset=0):
+        assert ev == ("finish", self.plies_run)
+        return self._ply_finish(on_moves, game_offset=game_offset)
+
     def _ply_finish(self, on_moves=None, refill=True, game_offset=0):
         self.plies_run += 1
         k = max(0, min(self.rate, self._limit - self.games_done))
