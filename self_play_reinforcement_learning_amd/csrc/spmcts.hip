@@ -1378,8 +1378,9 @@ __global__ __launch_bounds__(256) void k_dedup_insert(View v) {
 // so no entry a lane can still see, or renew, is taken by the other).  Tags never return to 0, so every entry
 // before a live key's entry in its probe chain has been in use since the key went in, and a lookup may stop at
 // the first never-used entry.  Publication: CAS to BUSY, key and outputs stored, then the READY tag stored with
-// release semantics (agent scope); lookups load tags with acquire semantics, so a READY key is never read torn
-// (a lane sharing its leader's table reads it while the leader's expand inserts on another stream).
+// release semantics (agent scope); a lookup confirms a candidate by acquire re-reads (cache_find), so a READY key
+// is never read torn (a lane sharing its leader's table reads it while the leader's expand inserts on another
+// stream).
 constexpr int CACHE_PROBES = 32;
 constexpr unsigned long long CACHE_READY = 1ull, CACHE_BUSY = 2ull;
 
